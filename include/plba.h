@@ -1,0 +1,141 @@
+/*
+ * plba.h — C ABI of the MI355X local-bundle-adjustment backend.
+ *
+ * Drop-in boundary for the g2o solve inside
+ *   void PLSLAM::MapHandler::localBundleAdjustmentForPlukerWithG2O()
+ *   (reference: include/mapHandler.h:134, src/mapHandler.cpp:5851-6323)
+ *
+ * The reference builds a g2o::SparseOptimizer on the stack (src/mapHandler.cpp:5923-5929),
+ * adds VertexLMPose / VertexLMPointXYZ / VertexLMLineOrth vertices and EdgePosePoint /
+ * EdgePoseLine edges (g2o_types/g2o_types.h:28-502), then runs
+ *   initializeOptimization(); optimize(5);  ... classify ...;
+ *   initializeOptimization(0); optimize(10);                     (src/mapHandler.cpp:6119-6152)
+ * Each entry point below replaces one of those g2o calls:
+ *
+ *   plba_create / plba_destroy        ~ g2o::SparseOptimizer ctor + setAlgorithm(Levenberg(BlockSolverX(
+ *                                       LinearSolverEigen)))  / dtor          (src/mapHandler.cpp:5923-5929)
+ *   plba_upload                       ~ addVertex / addEdge / setRobustKernel / SetParams loop
+ *                                                                              (src/mapHandler.cpp:5931-6117)
+ *   plba_set_edge_levels              ~ Edge::setLevel                        (src/mapHandler.cpp:6130,6143)
+ *   plba_set_robust                   ~ Edge::setRobustKernel(0 | Huber)      (src/mapHandler.cpp:6133,6146)
+ *   plba_initialize_optimization      ~ SparseOptimizer::initializeOptimization(int level)
+ *                                                                              (src/mapHandler.cpp:6121,6151)
+ *   plba_optimize                     ~ SparseOptimizer::optimize(int iterations)
+ *                                                                              (src/mapHandler.cpp:6122,6152)
+ *   plba_refresh_edge_errors          ~ Edge::computeError() on level-1 edges (src/mapHandler.cpp:6158-6160,6226-6228)
+ *   plba_get_edge_chi2                ~ Edge::chi2() / EdgePosePoint::isDepthPositive()
+ *                                                                              (src/mapHandler.cpp:6129,6142,6161,6230)
+ *   plba_download                     ~ Vertex::estimate()                    (src/mapHandler.cpp:6297-6319)
+ *   plba_lba_plucker                  the whole two-stage schedule of src/mapHandler.cpp:6119-6160 on device,
+ *                                     with no host round trip between the stages.
+ *
+ * Conventions: all arrays are host pointers owned by the caller and copied by the call;
+ * FP64 everywhere; indices are int32; every function returns PLBA_OK (0) or a negative
+ * PLBA_E* status and never throws or exits (the reference exit(0)s on index errors,
+ * src/mapHandler.cpp:5894,5910,5998,6062). A context is single-threaded (one LBA at a time,
+ * as handlerThread guarantees, src/mapHandler.cpp:1186-1188).
+ */
+#ifndef PLBA_H
+#define PLBA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PLBA_OK              0
+#define PLBA_E_INVALID     (-1)   /* bad argument / index out of range                 */
+#define PLBA_E_DEVICE      (-2)   /* HIP runtime error                                 */
+#define PLBA_E_STATE       (-3)   /* call out of order (e.g. optimize before upload)   */
+#define PLBA_E_NOMEM       (-4)
+#define PLBA_E_COMM        (-5)   /* RCCL error (sharded windows)                      */
+
+/* One LBA window in g2o vertex/edge form (structure-of-arrays).
+ * Vertex ids follow src/mapHandler.cpp:5941 (pose id = kf_idx), :5983 (point id =
+ * idx+max_kf_id+1), :6047 (line id = idx+maxPointId+1). Ids order the Hessian exactly as
+ * g2o's buildIndexMapping does (free poses by id, then landmarks by id). Edge arrays are in
+ * g2o insertion order (all point edges, then all line edges). */
+typedef struct plba_graph {
+    int32_t n_kf, n_pt, n_ln, n_ept, n_eln;
+    double fx, fy, cx, cy;            /* EdgePosePoint/EdgePoseLine::SetParams (g2o_types.h:217,313) */
+    const double  *kf_Tcw;            /* [n_kf][12]  row-major 3x4 [R | t] of Tcw = T_kf_w^-1     */
+    const uint8_t *kf_fixed;          /* [n_kf]      VertexLMPose::setFixed                        */
+    const int32_t *kf_id;             /* [n_kf]      vertex id                                     */
+    const double  *pt_xyz;            /* [n_pt][3]   VertexLMPointXYZ estimate                     */
+    const int32_t *pt_id;             /* [n_pt]                                                    */
+    const double  *ln_orth;           /* [n_ln][4]   VertexLMLineOrth estimate (θ1,θ2,θ3,φ)        */
+    const int32_t *ln_id;             /* [n_ln]                                                    */
+    const int32_t *ept_lm, *ept_kf;   /* [n_ept]     vertex 0 (point index) / vertex 1 (kf index)  */
+    const double  *ept_obs;           /* [n_ept][2]  pixel measurement                             */
+    const double  *ept_info;          /* [n_ept]     Ω = info·I2 (info already float-rounded)      */
+    const int32_t *eln_lm, *eln_kf;   /* [n_eln]                                                   */
+    const double  *eln_obs;           /* [n_eln][4]  (spl.x, spl.y, epl.x, epl.y)                  */
+    const double  *eln_info;          /* [n_eln]     Ω = info·I4                                   */
+    double huber_pt, huber_ln;        /* RobustKernelHuber::setDelta ((float)sqrt(5.991))          */
+} plba_graph;
+
+/* Per outer-LM-iteration trace (OptimizationAlgorithmLevenberg::solve). */
+typedef struct plba_iter_trace {
+    int32_t stage;        /* 0 or 1 (optimize(5) / optimize(10))                    */
+    int32_t iter;         /* iteration index inside optimize()                      */
+    int32_t trials;       /* damped trials run (1..10)                              */
+    int32_t result;       /* 0 OK, 1 Terminate, 2 Fail                              */
+    double  chi2_start;   /* activeRobustChi2 at linearisation                     */
+    double  chi2_end;     /* currentChi after the trial loop                        */
+    double  lambda_start; /* λ used by the first trial                              */
+    double  lambda_end;   /* λ after the trial loop                                 */
+} plba_iter_trace;
+
+/* Output of plba_lba_plucker (all optional; NULL = not wanted). */
+typedef struct plba_result {
+    double  *kf_Tcw;        /* [n_kf][12] final Tcw (fixed poses unchanged)                   */
+    double  *pt_xyz;        /* [n_pt][3]                                                       */
+    double  *ln_orth;       /* [n_ln][4]                                                       */
+    double  *ept_chi2;      /* [n_ept] chi2 as the post-solve outlier pass sees it (A13 rules) */
+    uint8_t *ept_depth_ok;  /* [n_ept] isDepthPositive() at the final state                    */
+    uint8_t *ept_level;     /* [n_ept] level after the stage-1 classification                  */
+    double  *eln_chi2;      /* [n_eln]                                                         */
+    uint8_t *eln_level;     /* [n_eln]                                                         */
+    int32_t  iters[2];      /* outer iterations executed by optimize(5) and optimize(10)      */
+    double   chi2[2];       /* final activeRobustChi2 of each stage                            */
+    double   solve_ms;      /* wall time inside the two optimize() calls                       */
+} plba_result;
+
+typedef struct plba_opts {
+    int32_t device;                  /* HIP device ordinal                                         */
+    int32_t corrected_line_jacobian; /* 0 = reproduce g2o_types.h:429-430 (orth used as Plücker)   */
+    int32_t verbose;                 /* print a per-iteration log to stderr                        */
+    int32_t max_trials;              /* g2o maxTrialsAfterFailure (10)                             */
+    double  tau;                     /* g2o Levenberg τ (1e-5)                                     */
+} plba_opts;
+
+typedef struct plba_ctx plba_ctx;
+
+void        plba_default_opts(plba_opts *o);
+int         plba_create(plba_ctx **ctx, const plba_opts *opts);
+int         plba_destroy(plba_ctx *ctx);
+const char *plba_last_error(const plba_ctx *ctx);
+
+int plba_upload(plba_ctx *ctx, const plba_graph *g);
+int plba_reset_estimates(plba_ctx *ctx);                       /* back to the uploaded estimates */
+int plba_set_edge_levels(plba_ctx *ctx, const uint8_t *ept_level, const uint8_t *eln_level);
+int plba_set_robust(plba_ctx *ctx, int32_t robust);            /* 1 = Huber on every edge, 0 = none */
+int plba_initialize_optimization(plba_ctx *ctx, int32_t level);
+int plba_optimize(plba_ctx *ctx, int32_t iterations, int32_t *iters_done, double *final_chi2);
+int plba_refresh_edge_errors(plba_ctx *ctx, int32_t level);    /* computeError() on edges of `level` */
+int plba_get_edge_chi2(plba_ctx *ctx, double *ept_chi2, uint8_t *ept_depth_ok, double *eln_chi2);
+int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth);
+int plba_lba_plucker(plba_ctx *ctx, plba_result *res);         /* full two-stage schedule          */
+int plba_get_trace(plba_ctx *ctx, plba_iter_trace *out, int32_t cap, int32_t *n);
+int plba_synchronize(plba_ctx *ctx);
+
+/* Per-kernel timing of the last plba_lba_plucker call (HIP events on the solver stream).
+ * names[i] points to a static string; ms[i] is the summed time of that kernel. */
+int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,
+                      int32_t cap, int32_t *n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLBA_H */

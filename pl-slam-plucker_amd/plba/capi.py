@@ -1,0 +1,131 @@
+"""ctypes mirror of include/plba.h (structs only; no library is loaded here)."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List
+
+import numpy as np
+
+from .synth import Graph
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+_bp = C.POINTER(C.c_uint8)
+
+
+class PlbaGraph(C.Structure):
+    _fields_ = [
+        ("n_kf", C.c_int32), ("n_pt", C.c_int32), ("n_ln", C.c_int32), ("n_ept", C.c_int32), ("n_eln", C.c_int32),
+        ("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+        ("kf_Tcw", _dp), ("kf_fixed", _bp), ("kf_id", _ip),
+        ("pt_xyz", _dp), ("pt_id", _ip),
+        ("ln_orth", _dp), ("ln_id", _ip),
+        ("ept_lm", _ip), ("ept_kf", _ip), ("ept_obs", _dp), ("ept_info", _dp),
+        ("eln_lm", _ip), ("eln_kf", _ip), ("eln_obs", _dp), ("eln_info", _dp),
+        ("huber_pt", C.c_double), ("huber_ln", C.c_double),
+    ]
+
+
+class PlbaIterTrace(C.Structure):
+    _fields_ = [("stage", C.c_int32), ("iter", C.c_int32), ("trials", C.c_int32), ("result", C.c_int32),
+                ("chi2_start", C.c_double), ("chi2_end", C.c_double),
+                ("lambda_start", C.c_double), ("lambda_end", C.c_double)]
+
+
+class PlbaResult(C.Structure):
+    _fields_ = [("kf_Tcw", _dp), ("pt_xyz", _dp), ("ln_orth", _dp),
+                ("ept_chi2", _dp), ("ept_depth_ok", _bp), ("ept_level", _bp),
+                ("eln_chi2", _dp), ("eln_level", _bp),
+                ("iters", C.c_int32 * 2), ("chi2", C.c_double * 2), ("solve_ms", C.c_double)]
+
+
+class PlbaOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("corrected_line_jacobian", C.c_int32), ("verbose", C.c_int32),
+                ("max_trials", C.c_int32), ("tau", C.c_double)]
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+class GraphView:
+    """Keeps contiguous copies of a Graph's arrays alive and exposes a PlbaGraph."""
+
+    def __init__(self, g: Graph):
+        self.keep: List[np.ndarray] = []
+
+        def f64(a, shape_last=None):
+            a = np.ascontiguousarray(a, dtype=np.float64)
+            self.keep.append(a)
+            return _ptr(a, _dp)
+
+        def i32(a):
+            a = np.ascontiguousarray(a, dtype=np.int32)
+            self.keep.append(a)
+            return _ptr(a, _ip)
+
+        def u8(a):
+            a = np.ascontiguousarray(a, dtype=np.uint8)
+            self.keep.append(a)
+            return _ptr(a, _bp)
+
+        s = PlbaGraph()
+        s.n_kf, s.n_pt, s.n_ln, s.n_ept, s.n_eln = g.n_kf, g.n_pt, g.n_ln, g.n_ept, g.n_eln
+        s.fx, s.fy, s.cx, s.cy = g.fx, g.fy, g.cx, g.cy
+        s.kf_Tcw = f64(g.kf_Tcw.reshape(-1, 12))
+        s.kf_fixed = u8(g.kf_fixed)
+        s.kf_id = i32(g.kf_id)
+        s.pt_xyz = f64(g.pt_xyz.reshape(-1, 3))
+        s.pt_id = i32(g.pt_id)
+        s.ln_orth = f64(g.ln_orth.reshape(-1, 4))
+        s.ln_id = i32(g.ln_id)
+        s.ept_lm, s.ept_kf = i32(g.ept_lm), i32(g.ept_kf)
+        s.ept_obs, s.ept_info = f64(g.ept_obs.reshape(-1, 2)), f64(g.ept_info)
+        s.eln_lm, s.eln_kf = i32(g.eln_lm), i32(g.eln_kf)
+        s.eln_obs, s.eln_info = f64(g.eln_obs.reshape(-1, 4)), f64(g.eln_info)
+        s.huber_pt, s.huber_ln = g.huber_pt, g.huber_ln
+        self.struct = s
+
+
+class ResultBuffers:
+    """Host output arrays for plba_result."""
+
+    def __init__(self, g: Graph):
+        self.kf_Tcw = np.zeros((g.n_kf, 3, 4))
+        self.pt_xyz = np.zeros((g.n_pt, 3))
+        self.ln_orth = np.zeros((g.n_ln, 4))
+        self.ept_chi2 = np.zeros(g.n_ept)
+        self.ept_depth_ok = np.zeros(g.n_ept, np.uint8)
+        self.ept_level = np.zeros(g.n_ept, np.uint8)
+        self.eln_chi2 = np.zeros(g.n_eln)
+        self.eln_level = np.zeros(g.n_eln, np.uint8)
+        r = PlbaResult()
+        r.kf_Tcw = _ptr(self.kf_Tcw, _dp)
+        r.pt_xyz = _ptr(self.pt_xyz, _dp)
+        r.ln_orth = _ptr(self.ln_orth, _dp)
+        r.ept_chi2 = _ptr(self.ept_chi2, _dp)
+        r.ept_depth_ok = _ptr(self.ept_depth_ok, _bp)
+        r.ept_level = _ptr(self.ept_level, _bp)
+        r.eln_chi2 = _ptr(self.eln_chi2, _dp)
+        r.eln_level = _ptr(self.eln_level, _bp)
+        self.struct = r
+
+    def as_dict(self) -> dict:
+        s = self.struct
+        return dict(kf_Tcw=self.kf_Tcw, pt_xyz=self.pt_xyz, ln_orth=self.ln_orth,
+                    ept_chi2=self.ept_chi2, ept_depth_ok=self.ept_depth_ok, ept_level=self.ept_level,
+                    eln_chi2=self.eln_chi2, eln_level=self.eln_level,
+                    iters=np.array([s.iters[0], s.iters[1]], np.int32),
+                    chi2=np.array([s.chi2[0], s.chi2[1]]), solve_ms=float(s.solve_ms))
+
+
+def trace_to_array(tr, n: int) -> np.ndarray:
+    """Structured numpy array from a PlbaIterTrace buffer."""
+    dt = np.dtype([("stage", np.int32), ("iter", np.int32), ("trials", np.int32), ("result", np.int32),
+                   ("chi2_start", np.float64), ("chi2_end", np.float64),
+                   ("lambda_start", np.float64), ("lambda_end", np.float64)])
+    out = np.zeros(n, dt)
+    for i in range(n):
+        t = tr[i]
+        out[i] = (t.stage, t.iter, t.trials, t.result, t.chi2_start, t.chi2_end, t.lambda_start, t.lambda_end)
+    return out

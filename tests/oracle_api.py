@@ -1,0 +1,133 @@
+"""TEST INFRASTRUCTURE: ctypes binding of the CPU oracle (oracle/librefcpu.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pl-slam-plucker_amd"))
+
+from plba import capi  # noqa: E402
+from plba.synth import Graph  # noqa: E402
+
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "librefcpu.so")
+
+
+class RefcpuOpts(C.Structure):
+    _fields_ = [("corrected_line_jacobian", C.c_int32), ("verbose", C.c_int32), ("max_trials", C.c_int32),
+                ("tau", C.c_double), ("stage_iters", C.c_int32 * 2)]
+
+
+_lib = None
+
+
+def build_oracle(force: bool = False) -> str:
+    src = os.path.join(ORACLE_DIR, "refcpu.cpp")
+    if force or not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", ORACLE_DIR, "-s"], check=True)
+    return ORACLE_SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build_oracle()
+        L = C.CDLL(ORACLE_SO)
+        dp = C.POINTER(C.c_double)
+        L.refcpu_default_opts.argtypes = [C.POINTER(RefcpuOpts)]
+        L.refcpu_lba_plucker.argtypes = [C.POINTER(capi.PlbaGraph), C.POINTER(RefcpuOpts), C.POINTER(capi.PlbaResult),
+                                         C.POINTER(capi.PlbaIterTrace), C.c_int32, C.POINTER(C.c_int32)]
+        L.refcpu_lba_plucker.restype = C.c_int
+        L.refcpu_point_edge.argtypes = [dp, dp, dp, C.c_double, C.c_double, C.c_double, C.c_double, dp, dp, dp]
+        L.refcpu_line_edge.argtypes = [dp, dp, dp, C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, dp, dp, dp]
+        L.refcpu_pose_oplus.argtypes = [dp, dp]
+        L.refcpu_line_oplus.argtypes = [dp, dp]
+        L.refcpu_orth_to_pluker.argtypes = [dp, dp]
+        L.refcpu_pluker_to_orth.argtypes = [dp, dp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def default_opts(**kw) -> RefcpuOpts:
+    o = RefcpuOpts()
+    lib().refcpu_default_opts(C.byref(o))
+    for k, v in kw.items():
+        if k == "stage_iters":
+            o.stage_iters[0], o.stage_iters[1] = v
+        else:
+            setattr(o, k, v)
+    return o
+
+
+def lba_plucker(g: Graph, **kw) -> dict:
+    """Run the full two-stage oracle LBA; returns final estimates, per-edge chi2, trace."""
+    gv = capi.GraphView(g)
+    rb = capi.ResultBuffers(g)
+    cap = 64
+    tr = (capi.PlbaIterTrace * cap)()
+    n = C.c_int32(0)
+    rc = lib().refcpu_lba_plucker(C.byref(gv.struct), C.byref(default_opts(**kw)), C.byref(rb.struct), tr, cap,
+                                  C.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"refcpu_lba_plucker failed: {rc}")
+    out = rb.as_dict()
+    out["trace"] = capi.trace_to_array(tr, min(n.value, cap))
+    return out
+
+
+def point_edge(Tcw, xyz, obs, cam):
+    Tcw = np.ascontiguousarray(Tcw, np.float64).reshape(12)
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    obs = np.ascontiguousarray(obs, np.float64)
+    e, Ji, Jj = np.zeros(2), np.zeros(6), np.zeros(12)
+    lib().refcpu_point_edge(_p(Tcw), _p(xyz), _p(obs), cam[0], cam[1], cam[2], cam[3], _p(e), _p(Ji), _p(Jj))
+    return e, Ji.reshape(2, 3), Jj.reshape(2, 6)
+
+
+def line_edge(Tcw, orth, obs, cam, corrected=0):
+    Tcw = np.ascontiguousarray(Tcw, np.float64).reshape(12)
+    orth = np.ascontiguousarray(orth, np.float64)
+    obs = np.ascontiguousarray(obs, np.float64)
+    e, Ji, Jj = np.zeros(4), np.zeros(16), np.zeros(24)
+    lib().refcpu_line_edge(_p(Tcw), _p(orth), _p(obs), cam[0], cam[1], cam[2], cam[3], corrected, _p(e), _p(Ji), _p(Jj))
+    return e, Ji.reshape(4, 4), Jj.reshape(4, 6)
+
+
+def pose_oplus(Tcw, d):
+    T = np.ascontiguousarray(Tcw, np.float64).reshape(12).copy()
+    d = np.ascontiguousarray(d, np.float64)
+    lib().refcpu_pose_oplus(_p(T), _p(d))
+    return T.reshape(3, 4)
+
+
+def line_oplus(orth, d):
+    o = np.ascontiguousarray(orth, np.float64).copy()
+    d = np.ascontiguousarray(d, np.float64)
+    lib().refcpu_line_oplus(_p(o), _p(d))
+    return o
+
+
+def orth_to_pluker(o):
+    o = np.ascontiguousarray(o, np.float64)
+    L = np.zeros(6)
+    lib().refcpu_orth_to_pluker(_p(o), _p(L))
+    return L
+
+
+def pluker_to_orth(L):
+    L = np.ascontiguousarray(L, np.float64)
+    o = np.zeros(4)
+    lib().refcpu_pluker_to_orth(_p(L), _p(o))
+    return o
