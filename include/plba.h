@@ -132,6 +132,7 @@ int plba_synchronize(plba_ctx *ctx);
 
 /* Per-kernel timing of the last plba_lba_plucker call (HIP events on the solver stream).
  * names[i] points to a static string; ms[i] is the summed time of that kernel. */
+int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on);   /* HIP-event timing of each launch */
 int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,
                       int32_t cap, int32_t *n);
 

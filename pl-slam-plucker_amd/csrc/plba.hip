@@ -1,0 +1,753 @@
+// plba.hip — host side of the MI355X LBA backend: context, structure preparation, the
+// Levenberg–Marquardt driver and the C ABI of include/plba.h.
+//
+// Control flow mirrors g2o exactly:
+//   SparseOptimizer::initializeOptimization(level)   -> plba_initialize_optimization
+//   SparseOptimizer::optimize(n)                     -> plba_optimize
+//     OptimizationAlgorithmLevenberg::solve(it)      -> one iteration launch + trial launches
+// The numerical work is all on the device (plba_kernels.hpp); the host only reads back the
+// 80-byte control block after each trial to decide whether another trial runs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/plba.h"
+#include "plba_kernels.hpp"
+
+namespace plba {
+
+#define PLBA_CHECK(expr)                                                                       \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) {                                                                \
+            ctx->set_error("HIP error %s at %s:%d: %s", hipGetErrorString(_e), __FILE__,       \
+                           __LINE__, #expr);                                                   \
+            return PLBA_E_DEVICE;                                                              \
+        }                                                                                      \
+    } while (0)
+
+enum KernelId {
+    K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_SCHUR, K_MEMSET, K_ASSEMBLE, K_FACTOR,
+    K_POSE_UPDATE, K_LM_UPDATE, K_DECIDE, K_COMMIT, K_COUNT
+};
+static const char *kKernelNames[K_COUNT] = {
+    "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_schur_landmark", "memset_rcs",
+    "k_rcs_assemble", "k_rcs_factor", "k_pose_update", "k_landmark_update", "k_decide", "k_commit"};
+
+}  // namespace plba
+
+using namespace plba;
+
+struct plba_ctx {
+    plba_opts opts;
+    std::string err;
+    hipStream_t stream = nullptr;
+    bool uploaded = false, initialized = false;
+    int level = 0;
+    int robust = 1;
+    Dev d{};
+    // device arena
+    std::vector<void *> allocs;
+    Ctrl *h_ctrl = nullptr;  // pinned
+    // host-side bookkeeping
+    int32_t n_kf = 0, n_pt = 0, n_ln = 0, Ep = 0, El = 0;
+    std::vector<int32_t> e_orig;        // CSR edge -> original index within its type
+    std::vector<uint8_t> h_level;       // [E] CSR order
+    std::vector<plba_iter_trace> trace;
+    int stage = 0;
+    size_t n_triples = 0;
+    // kernel timing (optional)
+    bool timing = false;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_next = 0;
+    double k_ms[K_COUNT] = {0};
+    int32_t k_n[K_COUNT] = {0};
+
+    void set_error(const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        if (opts.verbose) fprintf(stderr, "[plba] %s\n", buf);
+    }
+    void free_all() {
+        for (void *p : allocs) (void)hipFree(p);
+        allocs.clear();
+        d = Dev{};
+        uploaded = initialized = false;
+    }
+    template <typename T>
+    int alloc(T *&p, size_t count) {
+        p = nullptr;
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc((void **)&p, count * sizeof(T));
+        if (e != hipSuccess) {
+            set_error("hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
+            return PLBA_E_NOMEM;
+        }
+        allocs.push_back(p);
+        return PLBA_OK;
+    }
+    hipEvent_t next_event() {
+        if (ev_next == ev_pool.size()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            ev_pool.push_back(e);
+        }
+        return ev_pool[ev_next++];
+    }
+};
+
+namespace {
+
+inline int blocks_for(int n, int b = kBlock) { return (n + b - 1) / b; }
+
+// time a launch when kernel timing is enabled
+template <typename F>
+int timed(plba_ctx *ctx, int kid, F &&launch) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (ctx->timing) {
+        a = ctx->next_event();
+        b = ctx->next_event();
+        (void)hipEventRecord(a, ctx->stream);
+    }
+    launch();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        ctx->set_error("kernel %s launch failed: %s", kKernelNames[kid], hipGetErrorString(e));
+        return PLBA_E_DEVICE;
+    }
+    if (ctx->timing) {
+        (void)hipEventRecord(b, ctx->stream);
+        ctx->ev_used.push_back({kid, {a, b}});
+    }
+    return PLBA_OK;
+}
+
+#define LAUNCH(kid, ...)                                   \
+    do {                                                   \
+        int _rc = timed(ctx, kid, [&] { __VA_ARGS__; });   \
+        if (_rc) return _rc;                               \
+    } while (0)
+
+int collect_timing(plba_ctx *ctx) {
+    if (!ctx->timing) return PLBA_OK;
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    for (auto &u : ctx->ev_used) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, u.second.first, u.second.second);
+        ctx->k_ms[u.first] += ms;
+        ctx->k_n[u.first] += 1;
+    }
+    ctx->ev_used.clear();
+    ctx->ev_next = 0;
+    return PLBA_OK;
+}
+
+template <typename T>
+int upload_vec(plba_ctx *ctx, T *&dst, const std::vector<T> &src) {
+    int rc = ctx->alloc(dst, src.size());
+    if (rc) return rc;
+    if (!src.empty()) PLBA_CHECK(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return PLBA_OK;
+}
+
+// ------------------------------------------------------------------ upload / structure prep
+int do_upload(plba_ctx *ctx, const plba_graph *g) {
+    if (!g || g->n_kf < 0 || g->n_pt < 0 || g->n_ln < 0 || g->n_ept < 0 || g->n_eln < 0) {
+        ctx->set_error("invalid graph sizes");
+        return PLBA_E_INVALID;
+    }
+    if ((g->n_kf && (!g->kf_Tcw || !g->kf_fixed || !g->kf_id)) || (g->n_pt && (!g->pt_xyz || !g->pt_id)) ||
+        (g->n_ln && (!g->ln_orth || !g->ln_id)) ||
+        (g->n_ept && (!g->ept_lm || !g->ept_kf || !g->ept_obs || !g->ept_info)) ||
+        (g->n_eln && (!g->eln_lm || !g->eln_kf || !g->eln_obs || !g->eln_info))) {
+        ctx->set_error("null array in graph");
+        return PLBA_E_INVALID;
+    }
+    for (int e = 0; e < g->n_ept; ++e)
+        if (g->ept_lm[e] < 0 || g->ept_lm[e] >= g->n_pt || g->ept_kf[e] < 0 || g->ept_kf[e] >= g->n_kf) {
+            ctx->set_error("point edge %d references a missing vertex", e);
+            return PLBA_E_INVALID;
+        }
+    for (int e = 0; e < g->n_eln; ++e)
+        if (g->eln_lm[e] < 0 || g->eln_lm[e] >= g->n_ln || g->eln_kf[e] < 0 || g->eln_kf[e] >= g->n_kf) {
+            ctx->set_error("line edge %d references a missing vertex", e);
+            return PLBA_E_INVALID;
+        }
+    ctx->free_all();
+    const int n_kf = g->n_kf, n_pt = g->n_pt, n_ln = g->n_ln, Ep = g->n_ept, El = g->n_eln;
+    const int n_lm = n_pt + n_ln, E = Ep + El;
+    ctx->n_kf = n_kf; ctx->n_pt = n_pt; ctx->n_ln = n_ln; ctx->Ep = Ep; ctx->El = El;
+
+    // free poses ordered by vertex id (buildIndexMapping)
+    std::vector<int32_t> korder(n_kf);
+    std::iota(korder.begin(), korder.end(), 0);
+    std::stable_sort(korder.begin(), korder.end(), [&](int a, int b) { return g->kf_id[a] < g->kf_id[b]; });
+    std::vector<int32_t> kf_hidx(n_kf, -1);
+    int nf = 0;
+    for (int k : korder)
+        if (!g->kf_fixed[k]) kf_hidx[k] = nf++;
+
+    // landmark-major CSR (stable within a landmark = g2o insertion order)
+    std::vector<int32_t> lm_cnt(n_lm + 1, 0);
+    for (int e = 0; e < Ep; ++e) lm_cnt[g->ept_lm[e] + 1]++;
+    for (int e = 0; e < El; ++e) lm_cnt[n_pt + g->eln_lm[e] + 1]++;
+    std::vector<int32_t> lm_off(n_lm + 1, 0);
+    for (int l = 0; l < n_lm; ++l) lm_off[l + 1] = lm_off[l] + lm_cnt[l + 1];
+    std::vector<int32_t> fill(lm_off.begin(), lm_off.end() - 1);
+    std::vector<int32_t> e_lm(E), e_kf(E), e_hidx(E), e_orig(E);
+    std::vector<double> e_obs((size_t)E * 4, 0.0), e_info(E);
+    for (int e = 0; e < Ep; ++e) {
+        int l = g->ept_lm[e], pos = fill[l]++;
+        e_lm[pos] = l;
+        e_kf[pos] = g->ept_kf[e];
+        e_orig[pos] = e;
+        e_obs[(size_t)pos * 4] = g->ept_obs[2 * e];
+        e_obs[(size_t)pos * 4 + 1] = g->ept_obs[2 * e + 1];
+        e_info[pos] = g->ept_info[e];
+    }
+    for (int e = 0; e < El; ++e) {
+        int l = n_pt + g->eln_lm[e], pos = fill[l]++;
+        e_lm[pos] = l;
+        e_kf[pos] = g->eln_kf[e];
+        e_orig[pos] = e;
+        for (int k = 0; k < 4; ++k) e_obs[(size_t)pos * 4 + k] = g->eln_obs[4 * e + k];
+        e_info[pos] = g->eln_info[e];
+    }
+    for (int e = 0; e < E; ++e) e_hidx[e] = kf_hidx[e_kf[e]];
+    ctx->e_orig = e_orig;
+    ctx->h_level.assign(E, 0);
+
+    // free-pose-major edge lists (ascending CSR edge index)
+    std::vector<int32_t> pe_off(nf + 1, 0);
+    for (int e = 0; e < E; ++e)
+        if (e_hidx[e] >= 0) pe_off[e_hidx[e] + 1]++;
+    for (int h = 0; h < nf; ++h) pe_off[h + 1] += pe_off[h];
+    std::vector<int32_t> pe_list(pe_off[nf]);
+    {
+        std::vector<int32_t> f(pe_off.begin(), pe_off.end() - 1);
+        for (int e = 0; e < E; ++e)
+            if (e_hidx[e] >= 0) pe_list[f[e_hidx[e]]++] = e;
+    }
+
+    // reduced-camera block pattern + triples (e1 at pose i1 <= e2 at pose i2, same landmark)
+    std::map<std::pair<int, int>, int> blk_index;
+    std::vector<std::pair<int, int>> blocks;
+    for (int h = 0; h < nf; ++h) {
+        blk_index[{h, h}] = (int)blocks.size();
+        blocks.push_back({h, h});
+    }
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> blk_trip(nf);
+    std::vector<int32_t> lm_edges;
+    for (int l = 0; l < n_lm; ++l) {
+        lm_edges.clear();
+        for (int e = lm_off[l]; e < lm_off[l + 1]; ++e)
+            if (e_hidx[e] >= 0) lm_edges.push_back(e);
+        for (int a : lm_edges)
+            for (int b : lm_edges) {
+                int i1 = e_hidx[a], i2 = e_hidx[b];
+                if (i1 > i2) continue;
+                auto key = std::make_pair(i1, i2);
+                auto it = blk_index.find(key);
+                int bi;
+                if (it == blk_index.end()) {
+                    bi = (int)blocks.size();
+                    blk_index[key] = bi;
+                    blocks.push_back(key);
+                    blk_trip.emplace_back();
+                } else {
+                    bi = it->second;
+                }
+                blk_trip[bi].push_back({a, b});
+            }
+    }
+    const int nblk = (int)blocks.size();
+    std::vector<int32_t> blk_i1(nblk), blk_i2(nblk), blk_off(nblk + 1, 0), trip;
+    {
+        // order blocks by (i2, i1) for locality; triples keep landmark order
+        std::vector<int> ord(nblk);
+        std::iota(ord.begin(), ord.end(), 0);
+        std::sort(ord.begin(), ord.end(), [&](int a, int b) {
+            return blocks[a].second != blocks[b].second ? blocks[a].second < blocks[b].second
+                                                        : blocks[a].first < blocks[b].first;
+        });
+        size_t tot = 0;
+        for (auto &v : blk_trip) tot += v.size();
+        trip.reserve(tot * 2);
+        for (int k = 0; k < nblk; ++k) {
+            int b = ord[k];
+            blk_i1[k] = blocks[b].first;
+            blk_i2[k] = blocks[b].second;
+            for (auto &t : blk_trip[b]) { trip.push_back(t.first); trip.push_back(t.second); }
+            blk_off[k + 1] = (int32_t)(trip.size() / 2);
+        }
+        ctx->n_triples = tot;
+    }
+    // envelope of the lower triangle (per 6-row pose block: first pose block column)
+    const int n = 6 * nf;
+    const int ntiles = (n + kTile - 1) / kTile;
+    std::vector<int32_t> first_blk(nf);
+    for (int h = 0; h < nf; ++h) first_blk[h] = h;
+    for (int k = 0; k < nblk; ++k) first_blk[blk_i2[k]] = std::min(first_blk[blk_i2[k]], blk_i1[k]);
+    std::vector<int32_t> tile_first(std::max(ntiles, 1), 0), tile_last(std::max(ntiles, 1), 0);
+    for (int I = 0; I < ntiles; ++I) {
+        int f = I;
+        for (int r = I * kTile; r < std::min(n, (I + 1) * kTile); ++r) f = std::min(f, (6 * first_blk[r / 6]) / kTile);
+        tile_first[I] = f;
+    }
+    for (int K = 0; K < ntiles; ++K) {
+        int last = K;
+        for (int I = K; I < ntiles; ++I)
+            if (tile_first[I] <= K) last = I;
+        tile_last[K] = last;
+    }
+
+    // ---- device allocation
+    Dev &d = ctx->d;
+    d.n_kf = n_kf; d.n_pt = n_pt; d.n_ln = n_ln; d.n_lm = n_lm; d.Ep = Ep; d.El = El; d.E = E;
+    d.nf = nf; d.n = n; d.nblk = nblk; d.ntiles = ntiles;
+    d.corrected = ctx->opts.corrected_line_jacobian;
+    d.robust = 1;
+    d.cam = Cam{g->fx, g->fy, g->cx, g->cy};
+    d.huber_pt = g->huber_pt;
+    d.huber_ln = g->huber_ln;
+    d.tau = ctx->opts.tau;
+    d.n_lin_blocks = blocks_for(E);
+    d.n_lm_blocks = blocks_for(n_lm);
+    d.n_kf_blocks = blocks_for(n_kf);
+
+    std::vector<double> T((size_t)n_kf * 12), X((size_t)n_lm * 4, 0.0);
+    for (size_t i = 0; i < T.size(); ++i) T[i] = g->kf_Tcw[i];
+    for (int p = 0; p < n_pt; ++p)
+        for (int k = 0; k < 3; ++k) X[(size_t)p * 4 + k] = g->pt_xyz[3 * p + k];
+    for (int l = 0; l < n_ln; ++l)
+        for (int k = 0; k < 4; ++k) X[(size_t)(n_pt + l) * 4 + k] = g->ln_orth[4 * l + k];
+
+    int rc = 0;
+#define ALLOC(p, n_)        \
+    rc = ctx->alloc(p, n_); \
+    if (rc) return rc
+#define UPLOAD(p, v)            \
+    rc = upload_vec(ctx, p, v); \
+    if (rc) return rc
+    UPLOAD(d.T_init, T);
+    UPLOAD(d.T_cur, T);
+    ALLOC(d.T_trial, T.size());
+    UPLOAD(d.X_init, X);
+    UPLOAD(d.X_cur, X);
+    ALLOC(d.X_trial, X.size());
+    UPLOAD(d.kf_hidx, kf_hidx);
+    ALLOC(d.kf_active, n_kf);
+    UPLOAD(d.e_lm, e_lm);
+    UPLOAD(d.e_kf, e_kf);
+    UPLOAD(d.e_hidx, e_hidx);
+    UPLOAD(d.e_obs, e_obs);
+    UPLOAD(d.e_info, e_info);
+    ALLOC(d.e_level, E);
+    ALLOC(d.e_active, E);
+    UPLOAD(d.lm_off, lm_off);
+    ALLOC(d.lm_active, n_lm);
+    UPLOAD(d.pe_off, pe_off);
+    UPLOAD(d.pe_list, pe_list);
+    ALLOC(d.A, (size_t)E * 12);
+    ALLOC(d.cvec, (size_t)E * 2);
+    ALLOC(d.B, (size_t)E * 8);
+    ALLOC(d.chi2_last, E);
+    ALLOC(d.Hpp, (size_t)nf * 36);
+    ALLOC(d.bp, (size_t)nf * 6);
+    ALLOC(d.Hll, (size_t)n_lm * 10);
+    ALLOC(d.bl, (size_t)n_lm * 4);
+    ALLOC(d.Lc, (size_t)n_lm * 10);
+    ALLOC(d.gv, (size_t)n_lm * 4);
+    ALLOC(d.Z, (size_t)E * 8);
+    ALLOC(d.q, (size_t)E * 2);
+    ALLOC(d.xl, (size_t)n_lm * 4);
+    UPLOAD(d.blk_i1, blk_i1);
+    UPLOAD(d.blk_i2, blk_i2);
+    UPLOAD(d.blk_off, blk_off);
+    UPLOAD(d.trip, trip);
+    ALLOC(d.Ad, (size_t)n * n);
+    ALLOC(d.bs, n);
+    ALLOC(d.xp, n);
+    ALLOC(d.Wbuf, (size_t)std::max(n, 1) * kTile);
+    UPLOAD(d.tile_first, tile_first);
+    UPLOAD(d.tile_last, tile_last);
+    ALLOC(d.part_chi2, d.n_lin_blocks);
+    ALLOC(d.part_max, nf + d.n_lm_blocks);
+    ALLOC(d.part_lm, d.n_lm_blocks);
+    ALLOC(d.part_lms, d.n_lm_blocks);
+    ALLOC(d.part_ps, d.n_kf_blocks);
+    ALLOC(d.ctrl, 1);
+#undef ALLOC
+#undef UPLOAD
+    PLBA_CHECK(hipMemset(d.e_level, 0, E));
+    PLBA_CHECK(hipMemset(d.xp, 0, sizeof(double) * std::max(n, 1)));
+    PLBA_CHECK(hipMemset(d.xl, 0, sizeof(double) * std::max(n_lm, 1) * 4));
+    PLBA_CHECK(hipMemset(d.chi2_last, 0, sizeof(double) * std::max(E, 1)));
+    PLBA_CHECK(hipMemset(d.ctrl, 0, sizeof(Ctrl)));
+    PLBA_CHECK(hipDeviceSynchronize());
+    ctx->uploaded = true;
+    ctx->initialized = false;
+    return PLBA_OK;
+}
+
+int do_initialize(plba_ctx *ctx, int level) {
+    Dev &d = ctx->d;
+    d.robust = ctx->robust;
+    if (d.E > 0) hipLaunchKernelGGL(k_activate_edges, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d, level);
+    int nv = std::max(d.n_lm, d.n_kf);
+    if (nv > 0) hipLaunchKernelGGL(k_activate_vertices, dim3(blocks_for(nv)), dim3(kBlock), 0, ctx->stream, d);
+    PLBA_CHECK(hipGetLastError());
+    ctx->level = level;
+    ctx->initialized = true;
+    return PLBA_OK;
+}
+
+int read_ctrl(plba_ctx *ctx) {
+    PLBA_CHECK(hipMemcpyAsync(ctx->h_ctrl, ctx->d.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, ctx->stream));
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    return PLBA_OK;
+}
+
+// OptimizationAlgorithmLevenberg::solve(iteration). Returns 0 OK, 1 Terminate, <0 error.
+int lm_iteration(plba_ctx *ctx, int it) {
+    Dev &d = ctx->d;
+    hipStream_t s = ctx->stream;
+    const int max_trials = ctx->opts.max_trials;
+    if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+    if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kBlock), 0, s, d));
+    if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+    LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kBlock), 0, s, d, it));
+    const Ctrl &c = *ctx->h_ctrl;
+    for (;;) {
+        if (d.n_lm > 0) LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_schur_landmark, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+        if (d.n > 0) {
+            LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
+            LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_assemble, dim3(blocks_for(d.nblk * 64)), dim3(kBlock), 0, s, d));
+            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
+        } else {
+            int one = 1;
+            PLBA_CHECK(hipMemcpyAsync(&d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, s));
+        }
+        if (d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(d.n_kf_blocks), dim3(kBlock), 0, s, d));
+        if (d.n_lm > 0) LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_landmark_update, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+        LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d, max_trials));
+        int nv = std::max(d.n_lm, d.n_kf);
+        LAUNCH(K_COMMIT, hipLaunchKernelGGL(k_commit, dim3(blocks_for(std::max(nv, 1))), dim3(kBlock), 0, s, d));
+        int rc = read_ctrl(ctx);
+        if (rc) return rc;
+        if (c.broke) break;
+        if (!(c.rho < 0 && c.qmax < max_trials)) break;
+    }
+    int result = 0;
+    if (c.qmax == max_trials || c.rho == 0 || !std::isfinite(c.lambda)) result = 1;
+    ctx->trace.push_back(plba_iter_trace{ctx->stage, it, c.qmax, result, c.chi2_start, c.currentChi, c.lambda_start,
+                                         c.lambda});
+    if (ctx->opts.verbose)
+        fprintf(stderr, "[plba] stage %d it %d chi2 %.9g -> %.9g lambda %.6g trials %d\n", ctx->stage, it,
+                c.chi2_start, c.currentChi, c.lambda, c.qmax);
+    return result;
+}
+
+int do_optimize(plba_ctx *ctx, int iterations, int32_t *iters_done, double *final_chi2) {
+    Dev &d = ctx->d;
+    // g2o returns -1 without iterating when no vertex is free & active (_ivMap empty)
+    std::vector<uint8_t> lm_act(d.n_lm), kf_act(d.n_kf);
+    bool any = false;
+    {
+        if (d.n_lm) PLBA_CHECK(hipMemcpyAsync(lm_act.data(), d.lm_active, d.n_lm, hipMemcpyDeviceToHost, ctx->stream));
+        if (d.n_kf) PLBA_CHECK(hipMemcpyAsync(kf_act.data(), d.kf_active, d.n_kf, hipMemcpyDeviceToHost, ctx->stream));
+        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+        for (auto a : lm_act) any |= a != 0;
+        for (auto a : kf_act) any |= a != 0;
+    }
+    if (!any) {
+        if (iters_done) *iters_done = -1;
+        if (final_chi2) *final_chi2 = 0.0;
+        return PLBA_OK;
+    }
+    d.robust = ctx->robust;
+    int done = 0;
+    for (int it = 0; it < iterations; ++it) {
+        int r = lm_iteration(ctx, it);
+        if (r < 0) return r;
+        ++done;
+        if (r != 0) break;
+    }
+    if (iters_done) *iters_done = done;
+    if (final_chi2) *final_chi2 = ctx->h_ctrl->currentChi;
+    return PLBA_OK;
+}
+
+int launch_edges(plba_ctx *ctx, void (*k)(Dev, int), int arg) {
+    if (ctx->d.E > 0) hipLaunchKernelGGL(k, dim3(blocks_for(ctx->d.E)), dim3(kBlock), 0, ctx->stream, ctx->d, arg);
+    PLBA_CHECK(hipGetLastError());
+    return PLBA_OK;
+}
+
+}  // namespace
+
+// ==================================================================================== C ABI
+extern "C" {
+
+void plba_default_opts(plba_opts *o) {
+    if (!o) return;
+    o->device = 0;
+    o->corrected_line_jacobian = 0;
+    o->verbose = 0;
+    o->max_trials = 10;
+    o->tau = 1e-5;
+}
+
+int plba_create(plba_ctx **out, const plba_opts *opts) {
+    if (!out) return PLBA_E_INVALID;
+    *out = nullptr;
+    plba_ctx *ctx = new (std::nothrow) plba_ctx();
+    if (!ctx) return PLBA_E_NOMEM;
+    if (opts) ctx->opts = *opts;
+    else plba_default_opts(&ctx->opts);
+    if (ctx->opts.max_trials <= 0) ctx->opts.max_trials = 10;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        delete ctx;
+        return PLBA_E_DEVICE;
+    }
+    if (ctx->opts.device < 0 || ctx->opts.device >= ndev || hipSetDevice(ctx->opts.device) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_ctrl, sizeof(Ctrl), hipHostMallocDefault) != hipSuccess) {
+        delete ctx;
+        return PLBA_E_DEVICE;
+    }
+    std::memset(ctx->h_ctrl, 0, sizeof(Ctrl));
+    *out = ctx;
+    return PLBA_OK;
+}
+
+int plba_destroy(plba_ctx *ctx) {
+    if (!ctx) return PLBA_OK;
+    (void)hipSetDevice(ctx->opts.device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    ctx->free_all();
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return PLBA_OK;
+}
+
+const char *plba_last_error(const plba_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int plba_upload(plba_ctx *ctx, const plba_graph *g) {
+    if (!ctx) return PLBA_E_INVALID;
+    (void)hipSetDevice(ctx->opts.device);
+    ctx->robust = 1;
+    ctx->trace.clear();
+    return do_upload(ctx, g);
+}
+
+int plba_reset_estimates(plba_ctx *ctx) {
+    if (!ctx || !ctx->uploaded) return ctx ? PLBA_E_STATE : PLBA_E_INVALID;
+    Dev &d = ctx->d;
+    PLBA_CHECK(hipMemcpyAsync(d.T_cur, d.T_init, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToDevice, ctx->stream));
+    PLBA_CHECK(hipMemcpyAsync(d.X_cur, d.X_init, sizeof(double) * (size_t)d.n_lm * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    PLBA_CHECK(hipMemsetAsync(d.e_level, 0, std::max(d.E, 1), ctx->stream));
+    PLBA_CHECK(hipMemsetAsync(d.xp, 0, sizeof(double) * std::max(d.n, 1), ctx->stream));
+    PLBA_CHECK(hipMemsetAsync(d.xl, 0, sizeof(double) * std::max(d.n_lm, 1) * 4, ctx->stream));
+    PLBA_CHECK(hipMemsetAsync(d.chi2_last, 0, sizeof(double) * std::max(d.E, 1), ctx->stream));
+    std::fill(ctx->h_level.begin(), ctx->h_level.end(), 0);
+    ctx->robust = 1;
+    ctx->initialized = false;
+    ctx->trace.clear();
+    return PLBA_OK;
+}
+
+int plba_set_edge_levels(plba_ctx *ctx, const uint8_t *ept_level, const uint8_t *eln_level) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    const int E = ctx->d.E;
+    std::vector<uint8_t> lv(E, 0);
+    for (int e = 0; e < E; ++e) {
+        int o = ctx->e_orig[e];
+        bool is_pt = e < ctx->Ep;
+        lv[e] = is_pt ? (ept_level ? ept_level[o] : 0) : (eln_level ? eln_level[o] : 0);
+    }
+    ctx->h_level = lv;
+    if (E) PLBA_CHECK(hipMemcpy(ctx->d.e_level, lv.data(), E, hipMemcpyHostToDevice));
+    ctx->initialized = false;
+    return PLBA_OK;
+}
+
+int plba_set_robust(plba_ctx *ctx, int32_t robust) {
+    if (!ctx) return PLBA_E_INVALID;
+    ctx->robust = robust ? 1 : 0;
+    ctx->d.robust = ctx->robust;
+    return PLBA_OK;
+}
+
+int plba_initialize_optimization(plba_ctx *ctx, int32_t level) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    (void)hipSetDevice(ctx->opts.device);
+    return do_initialize(ctx, level);
+}
+
+int plba_optimize(plba_ctx *ctx, int32_t iterations, int32_t *iters_done, double *final_chi2) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (!ctx->uploaded || !ctx->initialized) return PLBA_E_STATE;
+    (void)hipSetDevice(ctx->opts.device);
+    int rc = do_optimize(ctx, iterations, iters_done, final_chi2);
+    ctx->stage++;
+    return rc;
+}
+
+int plba_refresh_edge_errors(plba_ctx *ctx, int32_t level) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    return launch_edges(ctx, k_refresh, level);
+}
+
+int plba_get_edge_chi2(plba_ctx *ctx, double *ept_chi2, uint8_t *ept_depth_ok, double *eln_chi2) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    Dev &d = ctx->d;
+    std::vector<double> chi(d.E);
+    std::vector<uint8_t> dep(d.Ep);
+    uint8_t *ddep = nullptr;
+    if (ept_depth_ok && d.Ep) {
+        PLBA_CHECK(hipMallocAsync((void **)&ddep, d.Ep, ctx->stream));
+        hipLaunchKernelGGL(k_depth, dim3(blocks_for(d.Ep)), dim3(kBlock), 0, ctx->stream, d, ddep);
+        PLBA_CHECK(hipGetLastError());
+        PLBA_CHECK(hipMemcpyAsync(dep.data(), ddep, d.Ep, hipMemcpyDeviceToHost, ctx->stream));
+        PLBA_CHECK(hipFreeAsync(ddep, ctx->stream));
+    }
+    if (d.E) PLBA_CHECK(hipMemcpyAsync(chi.data(), d.chi2_last, sizeof(double) * d.E, hipMemcpyDeviceToHost, ctx->stream));
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    for (int e = 0; e < d.E; ++e) {
+        int o = ctx->e_orig[e];
+        if (e < d.Ep) {
+            if (ept_chi2) ept_chi2[o] = chi[e];
+            if (ept_depth_ok) ept_depth_ok[o] = dep[e];
+        } else if (eln_chi2) {
+            eln_chi2[o] = chi[e];
+        }
+    }
+    return PLBA_OK;
+}
+
+int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    Dev &d = ctx->d;
+    std::vector<double> X((size_t)d.n_lm * 4);
+    if (kf_Tcw && d.n_kf)
+        PLBA_CHECK(hipMemcpyAsync(kf_Tcw, d.T_cur, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost, ctx->stream));
+    if (d.n_lm) PLBA_CHECK(hipMemcpyAsync(X.data(), d.X_cur, sizeof(double) * X.size(), hipMemcpyDeviceToHost, ctx->stream));
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    if (pt_xyz)
+        for (int p = 0; p < d.n_pt; ++p)
+            for (int k = 0; k < 3; ++k) pt_xyz[3 * p + k] = X[(size_t)p * 4 + k];
+    if (ln_orth)
+        for (int l = 0; l < d.n_ln; ++l)
+            for (int k = 0; k < 4; ++k) ln_orth[4 * l + k] = X[(size_t)(d.n_pt + l) * 4 + k];
+    return PLBA_OK;
+}
+
+// The whole schedule of src/mapHandler.cpp:6119-6160 (stage 1, classification, stage 2,
+// level-1 refresh) with no host round trip except the per-trial control read.
+int plba_lba_plucker(plba_ctx *ctx, plba_result *res) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    (void)hipSetDevice(ctx->opts.device);
+    Dev &d = ctx->d;
+    ctx->trace.clear();
+    for (int k = 0; k < K_COUNT; ++k) { ctx->k_ms[k] = 0; ctx->k_n[k] = 0; }
+    auto t0 = std::chrono::steady_clock::now();
+    int rc;
+    int it1 = 0, it2 = 0;
+    double chi1 = 0, chi2 = 0;
+    // stage 1: all edges level 0, Huber on
+    ctx->robust = 1;
+    ctx->stage = 0;
+    if ((rc = do_initialize(ctx, 0))) return rc;
+    if ((rc = do_optimize(ctx, 5, &it1, &chi1))) return rc;
+    // classification: chi2 > 5.991 || depth <= 0 -> level 1; kernels removed
+    if (d.E > 0) hipLaunchKernelGGL(k_classify, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d, 5.991);
+    PLBA_CHECK(hipGetLastError());
+    ctx->robust = 0;
+    // stage 2
+    ctx->stage = 1;
+    if ((rc = do_initialize(ctx, 0))) return rc;
+    if ((rc = do_optimize(ctx, 10, &it2, &chi2))) return rc;
+    // computeError() on the level-1 edges at the final state
+    if ((rc = launch_edges(ctx, k_refresh, 1))) return rc;
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    auto t1 = std::chrono::steady_clock::now();
+    if ((rc = collect_timing(ctx))) return rc;
+    if (res) {
+        res->iters[0] = it1;
+        res->iters[1] = it2;
+        res->chi2[0] = chi1;
+        res->chi2[1] = chi2;
+        res->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if ((rc = plba_download(ctx, res->kf_Tcw, res->pt_xyz, res->ln_orth))) return rc;
+        if (res->ept_chi2 || res->ept_depth_ok || res->eln_chi2)
+            if ((rc = plba_get_edge_chi2(ctx, res->ept_chi2, res->ept_depth_ok, res->eln_chi2))) return rc;
+        if (res->ept_level || res->eln_level) {
+            std::vector<uint8_t> lv(d.E);
+            if (d.E) PLBA_CHECK(hipMemcpy(lv.data(), d.e_level, d.E, hipMemcpyDeviceToHost));
+            for (int e = 0; e < d.E; ++e) {
+                int o = ctx->e_orig[e];
+                if (e < d.Ep) { if (res->ept_level) res->ept_level[o] = lv[e]; }
+                else if (res->eln_level) res->eln_level[o] = lv[e];
+            }
+        }
+    }
+    return PLBA_OK;
+}
+
+int plba_get_trace(plba_ctx *ctx, plba_iter_trace *out, int32_t cap, int32_t *n) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (n) *n = (int32_t)ctx->trace.size();
+    if (out)
+        for (int i = 0; i < (int)ctx->trace.size() && i < cap; ++i) out[i] = ctx->trace[i];
+    return PLBA_OK;
+}
+
+int plba_synchronize(plba_ctx *ctx) {
+    if (!ctx) return PLBA_E_INVALID;
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    return PLBA_OK;
+}
+
+int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches, int32_t cap, int32_t *n) {
+    if (!ctx) return PLBA_E_INVALID;
+    if (n) *n = K_COUNT;
+    for (int k = 0; k < K_COUNT && k < cap; ++k) {
+        if (names) names[k] = kKernelNames[k];
+        if (ms) ms[k] = ctx->k_ms[k];
+        if (launches) launches[k] = ctx->k_n[k];
+    }
+    return PLBA_OK;
+}
+
+// Extension: enable per-kernel HIP-event timing for subsequent plba_lba_plucker calls.
+int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on) {
+    if (!ctx) return PLBA_E_INVALID;
+    ctx->timing = on != 0;
+    return PLBA_OK;
+}
+
+}  // extern "C"

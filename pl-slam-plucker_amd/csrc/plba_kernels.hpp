@@ -1,0 +1,824 @@
+// plba_kernels.hpp — HIP kernels of the LM solve (gfx950, FP64, wave64).
+//
+// Per LM outer iteration (OptimizationAlgorithmLevenberg::solve):
+//   k_linearize        edge-parallel: error, χ², Huber weight, weighted Jacobians
+//                      (computeActiveErrors + linearizeOplus + constructQuadraticForm, A5/A6/A9/A10)
+//   k_pose_reduce      pose-parallel deterministic segmented sum: Hpp, b_p
+//   k_landmark_reduce  landmark-parallel: Hll, b_l; max|diag| partials
+//   k_iter_init        χ²_cur, λ init (τ·max|H_jj|, iteration 0)
+// Per damped trial:
+//   k_schur_landmark   (Hll+λI) = LLᵀ per landmark; Z_e = B_e L⁻ᵀ, q_e = Z_e L⁻¹ b_l
+//   k_rcs_assemble     one wave per reduced-camera block: Hpp+λI − Σ A₁ᵀ(Z₁Z₂ᵀ)A₂ ; b_s
+//   k_rcs_factor       one workgroup: envelope-aware tiled LDLᵀ + solve (LinearSolverEigen)
+//   k_pose_update      oplus of the free poses, scale partials
+//   k_landmark_update  back-substitution, oplus, trial χ² of every active edge
+//   k_decide           ρ, accept/reject, λ/ν update (g2o Levenberg rules)
+//   k_commit           trial -> current on accept (push/pop/discardTop)
+// All reductions are fixed-order trees: results are bitwise reproducible run to run.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "plba_math.hpp"
+
+namespace plba {
+
+constexpr int kBlock = 256;
+constexpr int kTile = 32;   // RCS factorisation tile
+
+struct Ctrl {
+    double lambda, ni, currentChi, tempChi, rho, scale, maxdiag;
+    double chi2_start, lambda_start;
+    int32_t qmax, accept, solve_ok, broke;
+    int32_t pad[4];
+};
+
+// All device pointers of one window (passed by value to every kernel).
+struct Dev {
+    int32_t n_kf, n_pt, n_ln, n_lm, Ep, El, E, nf, n;
+    int32_t corrected, robust, n_lin_blocks, n_lm_blocks, n_kf_blocks, nblk, ntiles;
+    Cam cam;
+    double huber_pt, huber_ln, tau;
+    // state
+    double *T_cur, *T_trial, *T_init;   // [n_kf][12]
+    double *X_cur, *X_trial, *X_init;   // [n_lm][4]
+    int32_t *kf_hidx;                   // [n_kf]
+    uint8_t *kf_active;                 // [n_kf]
+    // edges, landmark-major CSR order (points first, then lines)
+    int32_t *e_lm, *e_kf, *e_hidx;      // [E]
+    double *e_obs;                      // [E][4]
+    double *e_info;                     // [E]
+    uint8_t *e_level, *e_active;        // [E]
+    int32_t *lm_off;                    // [n_lm+1]
+    uint8_t *lm_active;                 // [n_lm]
+    int32_t *pe_off, *pe_list;          // free-pose-major edge lists [nf+1], [..]
+    // linearisation
+    double *A, *cvec, *B, *chi2_last;   // [E][12], [E][2], [E][8], [E]
+    double *Hpp, *bp;                   // [nf][36], [nf][6]
+    double *Hll, *bl;                   // [n_lm][10], [n_lm][4]
+    // Schur
+    double *Lc, *gv, *Z, *q, *xl;       // [n_lm][10], [n_lm][4], [E][8], [E][2], [n_lm][4]
+    // reduced camera system
+    int32_t *blk_i1, *blk_i2, *blk_off; // [nblk], [nblk], [nblk+1]
+    int32_t *trip;                      // [T][2]
+    double *Ad, *bs, *xp, *Wbuf;        // [n*n], [n], [n], [n*kTile]
+    int32_t *tile_first;                // [ntiles] first nonzero column tile of each row tile
+    int32_t *tile_last;                 // [ntiles] last row tile whose envelope reaches column tile K
+    // reductions
+    double *part_chi2;                  // [n_lin_blocks]
+    double *part_max;                   // [nf + n_lm_blocks]
+    double *part_lm, *part_lms;         // [n_lm_blocks]
+    double *part_ps;                    // [n_kf_blocks]
+    Ctrl *ctrl;
+};
+
+// ---------------------------------------------------------------- block reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) v = fmax(v, __shfl_xor(v, m, 64));
+    return v;
+}
+// deterministic block sum: xor-butterfly inside each wave, then waves in index order.
+// `sh` needs NT/64 doubles. Every thread receives the result.
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double *sh) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = sh[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) r += sh[w];
+    __syncthreads();
+    return r;
+}
+template <int NT>
+__device__ __forceinline__ double block_max(double v, double *sh) {
+    v = wave_max(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = sh[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) r = fmax(r, sh[w]);
+    __syncthreads();
+    return r;
+}
+__device__ __forceinline__ bool is_point_lm(const Dev &d, int lm) { return lm < d.n_pt; }
+
+// ---------------------------------------------------------------- activation
+__global__ void k_activate_edges(Dev d, int level) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < d.E) d.e_active[e] = (d.e_level[e] == level) ? 1 : 0;
+}
+__global__ void k_activate_vertices(Dev d) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d.n_lm) {
+        uint8_t a = 0;
+        for (int e = d.lm_off[i]; e < d.lm_off[i + 1]; ++e) a |= d.e_active[e];
+        d.lm_active[i] = a;
+    }
+    if (i < d.n_kf) {
+        int h = d.kf_hidx[i];
+        uint8_t a = 0;
+        if (h >= 0)
+            for (int p = d.pe_off[h]; p < d.pe_off[h + 1]; ++p) a |= d.e_active[d.pe_list[p]];
+        d.kf_active[i] = a;
+    }
+}
+
+// ---------------------------------------------------------------- linearisation
+__global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
+    __shared__ double sh[kBlock / 64];
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    double rc = 0.0;
+    if (e < d.E) {
+        double *A = d.A + (size_t)e * 12, *c = d.cvec + (size_t)e * 2, *B = d.B + (size_t)e * 8;
+        if (d.e_active[e]) {
+            const int lm = d.e_lm[e], kf = d.e_kf[e];
+            const double *T = d.T_cur + (size_t)kf * 12;
+            const double *X = d.X_cur + (size_t)lm * 4;
+            const double *obs = d.e_obs + (size_t)e * 4;
+            double err[2], Jl[8], Jp[12];
+            double delta;
+            if (e < d.Ep) {
+                double z;
+                point_error(T, X, obs, d.cam, err, z);
+                point_jac(T, X, d.cam, Jl, Jp);
+                // widen 2x3 -> 2x4
+                Jl[7] = 0; Jl[6] = Jl[5]; Jl[5] = Jl[4]; Jl[4] = Jl[3]; Jl[3] = 0;
+                delta = d.huber_pt;
+            } else {
+                double L[6];
+                orth_to_pluker(X, L);
+                line_jac(T, X, L, obs, d.cam, d.corrected, err, Jl, Jp);
+                delta = d.huber_ln;
+            }
+            const double info = d.e_info[e];
+            const double chi = err[0] * (info * err[0]) + err[1] * (info * err[1]);
+            d.chi2_last[e] = chi;
+            double rho0 = chi, rho1 = 1.0;
+            if (d.robust) huber(chi, delta, rho0, rho1);
+            rc = rho0;
+            const double s = sqrt(rho1 * info);
+            const bool pose_free = d.e_hidx[e] >= 0;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) A[k] = pose_free ? s * Jp[k] : 0.0;
+            c[0] = -s * err[0];
+            c[1] = -s * err[1];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) B[k] = s * Jl[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) A[k] = 0.0;
+            c[0] = c[1] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) B[k] = 0.0;
+        }
+    }
+    double s = block_sum<kBlock>(rc, sh);
+    if (threadIdx.x == 0) d.part_chi2[blockIdx.x] = s;
+}
+
+// one workgroup per free pose: Hpp = Σ AᵀA, b_p = Σ Aᵀc (deterministic)
+__global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
+    const int h = blockIdx.x;
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+    for (int p = d.pe_off[h] + threadIdx.x; p < d.pe_off[h + 1]; p += kBlock) {
+        const int e = d.pe_list[p];
+        const double *A = d.A + (size_t)e * 12;
+        const double *c = d.cvec + (size_t)e * 2;
+        double a0[6], a1[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { a0[k] = A[k]; a1[k] = A[6 + k]; }
+        const double c0 = c[0], c1 = c[1];
+        int idx = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int cc = r; cc < 6; ++cc) acc[idx++] += a0[r] * a0[cc] + a1[r] * a1[cc];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) acc[21 + r] += a0[r] * c0 + a1[r] * c1;
+    }
+    __shared__ double sh27[kBlock / 64][27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) acc[k] = wave_sum(acc[k]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < 27; ++k) sh27[threadIdx.x >> 6][k] = acc[k];
+    __syncthreads();
+    double out[27];
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 27; ++k) {
+            double v = sh27[0][k];
+            for (int w = 1; w < kBlock / 64; ++w) v += sh27[w][k];
+            out[k] = v;
+        }
+    if (threadIdx.x == 0) {
+        double *H = d.Hpp + (size_t)h * 36;
+        int idx = 0;
+        double mx = 0.0;
+        for (int r = 0; r < 6; ++r)
+            for (int cc = r; cc < 6; ++cc) {
+                H[r * 6 + cc] = out[idx];
+                H[cc * 6 + r] = out[idx];
+                if (r == cc) mx = fmax(mx, fabs(out[idx]));
+                ++idx;
+            }
+        for (int r = 0; r < 6; ++r) d.bp[(size_t)h * 6 + r] = out[21 + r];
+        d.part_max[h] = mx;
+    }
+}
+
+// packed lower-triangular index for 4x4 symmetric
+__device__ __forceinline__ constexpr int pk(int r, int c) { return r * (r + 1) / 2 + c; }
+
+__global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
+    __shared__ double sh[kBlock / 64];
+    const int l = blockIdx.x * kBlock + threadIdx.x;
+    double mx = 0.0;
+    if (l < d.n_lm) {
+        double H[10], b[4];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) H[k] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b[k] = 0.0;
+        for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
+            const double *B = d.B + (size_t)e * 8;
+            const double *c = d.cvec + (size_t)e * 2;
+            double b0[4], b1[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { b0[k] = B[k]; b1[k] = B[4 + k]; }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int cc = 0; cc <= r; ++cc) H[pk(r, cc)] += b0[r] * b0[cc] + b1[r] * b1[cc];
+                b[r] += b0[r] * c[0] + b1[r] * c[1];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 10; ++k) d.Hll[(size_t)l * 10 + k] = H[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d.bl[(size_t)l * 4 + k] = b[k];
+        mx = fmax(fmax(fabs(H[pk(0, 0)]), fabs(H[pk(1, 1)])), fmax(fabs(H[pk(2, 2)]), fabs(H[pk(3, 3)])));
+    }
+    double m = block_max<kBlock>(mx, sh);
+    if (threadIdx.x == 0) d.part_max[d.nf + blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(kBlock) void k_iter_init(Dev d, int iteration) {
+    __shared__ double sh[kBlock / 64];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) s += d.part_chi2[i];
+    double chi = block_sum<kBlock>(s, sh);
+    double m = 0.0;
+    for (int i = threadIdx.x; i < d.nf + d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[i]);
+    double mx = block_max<kBlock>(m, sh);
+    if (threadIdx.x == 0) {
+        Ctrl *c = d.ctrl;
+        c->currentChi = chi;
+        c->chi2_start = chi;
+        if (iteration == 0) {
+            c->maxdiag = mx;
+            c->lambda = d.tau * mx;
+            c->ni = 2.0;
+        }
+        c->lambda_start = c->lambda;
+        c->qmax = 0;
+        c->accept = 0;
+        c->rho = 0.0;
+        c->broke = 0;
+    }
+}
+
+// ---------------------------------------------------------------- Schur, per landmark
+template <int DIM>
+__device__ __forceinline__ void schur_landmark(const Dev &d, int l, double lam) {
+    double H[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) H[k] = d.Hll[(size_t)l * 10 + k];
+    // Cholesky of D = Hll + λI (DIM x DIM), packed lower
+    double L[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) L[k] = 0.0;
+#pragma unroll
+    for (int j = 0; j < DIM; ++j) {
+        double s = H[pk(j, j)] + lam;
+#pragma unroll
+        for (int p = 0; p < j; ++p) s -= L[pk(j, p)] * L[pk(j, p)];
+        const double djj = sqrt(s);
+        L[pk(j, j)] = djj;
+#pragma unroll
+        for (int i = j + 1; i < DIM; ++i) {
+            double t = H[pk(i, j)];
+#pragma unroll
+            for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
+            L[pk(i, j)] = t / djj;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) d.Lc[(size_t)l * 10 + k] = L[k];
+    // g = L^-1 b_l
+    double g[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < DIM; ++i) {
+        double t = d.bl[(size_t)l * 4 + i];
+#pragma unroll
+        for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * g[p];
+        g[i] = t / L[pk(i, i)];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d.gv[(size_t)l * 4 + k] = g[k];
+    for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
+        const double *B = d.B + (size_t)e * 8;
+        double z[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int i = 0; i < DIM; ++i) {
+                double t = B[r * 4 + i];
+#pragma unroll
+                for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * z[r][p];
+                z[r][i] = t / L[pk(i, i)];
+            }
+        double *Z = d.Z + (size_t)e * 8;
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Z[r * 4 + i] = z[r][i];
+        double q0 = 0, q1 = 0;
+#pragma unroll
+        for (int i = 0; i < DIM; ++i) { q0 += z[0][i] * g[i]; q1 += z[1][i] * g[i]; }
+        d.q[(size_t)e * 2 + 0] = q0;
+        d.q[(size_t)e * 2 + 1] = q1;
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_schur_landmark(Dev d) {
+    const int l = blockIdx.x * kBlock + threadIdx.x;
+    if (l >= d.n_lm) return;
+    const double lam = d.ctrl->lambda;
+    if (is_point_lm(d, l)) schur_landmark<3>(d, l, lam);
+    else schur_landmark<4>(d, l, lam);
+}
+
+// ---------------------------------------------------------------- reduced camera system
+// one wave per block (i1 <= i2): H = [i1==i2](Hpp + λI) − Σ_triples A₁ᵀ (Z₁ Z₂ᵀ) A₂
+__global__ __launch_bounds__(kBlock) void k_rcs_assemble(Dev d) {
+    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave >= d.nblk) return;
+    const int i1 = d.blk_i1[wave], i2 = d.blk_i2[wave];
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+    for (int t = d.blk_off[wave] + lane; t < d.blk_off[wave + 1]; t += 64) {
+        const int e1 = d.trip[2 * t], e2 = d.trip[2 * t + 1];
+        const double *Z1 = d.Z + (size_t)e1 * 8, *Z2 = d.Z + (size_t)e2 * 8;
+        const double *A1 = d.A + (size_t)e1 * 12, *A2 = d.A + (size_t)e2 * 12;
+        double z1[8], z2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { z1[k] = Z1[k]; z2[k] = Z2[k]; }
+        double m00 = 0, m01 = 0, m10 = 0, m11 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            m00 += z1[k] * z2[k];
+            m01 += z1[k] * z2[4 + k];
+            m10 += z1[4 + k] * z2[k];
+            m11 += z1[4 + k] * z2[4 + k];
+        }
+        double a2[12], Q[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) a2[k] = A2[k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            Q[k] = m00 * a2[k] + m01 * a2[6 + k];
+            Q[6 + k] = m10 * a2[k] + m11 * a2[6 + k];
+        }
+        double a1[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) a1[k] = A1[k];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) acc[r * 6 + c] += a1[r] * Q[c] + a1[6 + r] * Q[6 + c];
+    }
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = wave_sum(acc[k]);
+    const int n = d.n;
+    const double lam = d.ctrl->lambda;
+    if (i1 == i2) {
+        // b_s = b_p − Σ_{e at pose} A_eᵀ q_e
+        double bacc[6] = {0, 0, 0, 0, 0, 0};
+        for (int p = d.pe_off[i1] + lane; p < d.pe_off[i1 + 1]; p += 64) {
+            const int e = d.pe_list[p];
+            const double *A = d.A + (size_t)e * 12;
+            const double q0 = d.q[(size_t)e * 2], q1 = d.q[(size_t)e * 2 + 1];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) bacc[r] += A[r] * q0 + A[6 + r] * q1;
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) bacc[r] = wave_sum(bacc[r]);
+        if (lane < 36) {
+            const int r = lane / 6, c = lane % 6;
+            double v;
+            // select acc[lane] with a static index (avoid scratch)
+            v = 0.0;
+#pragma unroll
+            for (int k = 0; k < 36; ++k) v = (k == lane) ? acc[k] : v;
+            double h = d.Hpp[(size_t)i1 * 36 + lane] - v;
+            if (r == c) h += lam;
+            d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
+        }
+        if (lane < 6) {
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) v = (k == lane) ? bacc[k] : v;
+            d.bs[6 * i1 + lane] = d.bp[(size_t)i1 * 6 + lane] - v;
+        }
+    } else if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < 36; ++k) v = (k == lane) ? acc[k] : v;
+        // block (i1,i2) row r of i1, col c of i2  -> lower position (6 i2 + c, 6 i1 + r)
+        d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -v;
+    }
+}
+
+// Envelope-aware tiled LDLᵀ of the lower triangle + solve, one workgroup of 1024 threads.
+// Semantics of Eigen::SimplicialLDLT as used by LinearSolverEigen: fails iff a pivot is 0.
+constexpr int kFacThreads = 1024;
+__global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
+    __shared__ double T[kTile][kTile + 1];
+    __shared__ double Dk[kTile];
+    __shared__ int s_fail;
+    const int tid = threadIdx.x;
+    const int n = d.n;
+    double *Ad = d.Ad;
+    if (tid == 0) s_fail = 0;
+    const int nt = d.ntiles;
+    for (int K = 0; K < nt; ++K) {
+        const int k0 = K * kTile;
+        const int kb = min(kTile, n - k0);
+        __syncthreads();
+        {   // load diagonal tile
+            const int r = tid >> 5, c = tid & 31;
+            if (r < kb && c <= r) T[r][c] = Ad[(size_t)(k0 + r) + (size_t)(k0 + c) * n];
+        }
+        __syncthreads();
+        for (int j = 0; j < kb; ++j) {
+            const int r = tid >> 5, c = tid & 31;
+            const double djj = T[j][j];
+            if (djj == 0.0) {
+                if (tid == 0) s_fail = 1;
+            } else if (r > j && c > j && c <= r && r < kb) {
+                T[r][c] -= (T[r][j] / djj) * T[c][j];
+            }
+            __syncthreads();
+        }
+        if (s_fail) break;
+        {   // L = T / D, store to global
+            const int r = tid >> 5, c = tid & 31;
+            if (r < kb && c < r) {
+                const double l = T[r][c] / T[c][c];
+                Ad[(size_t)(k0 + r) + (size_t)(k0 + c) * n] = l;
+            }
+            if (tid < kb) {
+                Dk[tid] = T[tid][tid];
+                Ad[(size_t)(k0 + tid) + (size_t)(k0 + tid) * n] = T[tid][tid];
+            }
+        }
+        __syncthreads();
+        {   // convert T strict lower to L (in LDS)
+            const int r = tid >> 5, c = tid & 31;
+            double l = 0.0;
+            if (r < kb && c < r) l = T[r][c] / Dk[c];
+            __syncthreads();
+            if (r < kb && c < r) T[r][c] = l;
+        }
+        __syncthreads();
+        // panel rows: i >= k0+kb with tile_first[tile(i)] <= K
+        const int rows0 = k0 + kb;
+        const int rows_end = min(n, (d.tile_last[K] + 1) * kTile);
+        for (int i = rows0 + tid; i < rows_end; i += kFacThreads) {
+            if (d.tile_first[i / kTile] > K) continue;
+            double *w = d.Wbuf + (size_t)i * kTile;   // W = L·D for this row (re-read by the update)
+            for (int c = 0; c < kb; ++c) {
+                double a = Ad[(size_t)i + (size_t)(k0 + c) * n];
+                for (int p = 0; p < c; ++p) a -= w[p] * T[c][p];
+                w[c] = a;
+                Ad[(size_t)i + (size_t)(k0 + c) * n] = a / Dk[c];
+            }
+        }
+        __syncthreads();
+        // trailing update: A[i][j] -= Σ_c W[i][c] L[j][c], for rows/cols in the panel, j <= i
+        const int m = n - rows0;
+        if (m > 0) {
+            // iterate over trailing tiles (I, J) with K < J <= I, both in the envelope of K
+            for (int I = K + 1; I <= d.tile_last[K]; ++I) {
+                if (d.tile_first[I] > K) continue;
+                for (int J = K + 1; J <= I; ++J) {
+                    if (d.tile_first[J] > K) continue;
+                    const int r = tid >> 5, c = tid & 31;
+                    const int i = I * kTile + r, j = J * kTile + c;
+                    if (i < n && j < n && j <= i) {
+                        double s = 0.0;
+                        for (int p = 0; p < kb; ++p)
+                            s += d.Wbuf[(size_t)i * kTile + p] * Ad[(size_t)j + (size_t)(k0 + p) * n];
+                        Ad[(size_t)i + (size_t)j * n] -= s;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
+    if (s_fail) return;  // x_p keeps its previous value (g2o leaves _x untouched on failure)
+    // ---- solve L D Lᵀ x = b_s
+    double *y = d.Wbuf;  // reuse: y[0..n)
+    for (int i = tid; i < n; i += kFacThreads) y[i] = d.bs[i];
+    __syncthreads();
+    // forward: tile by tile
+    for (int K = 0; K < nt; ++K) {
+        const int k0 = K * kTile, kb = min(kTile, n - k0);
+        if (tid < 64) {  // one wave solves the diagonal tile
+            double yi = (tid < kb) ? y[k0 + tid] : 0.0;
+            for (int j = 0; j < kb; ++j) {
+                const double yj = __shfl(yi, j, 64);
+                if (tid > j && tid < kb) yi -= Ad[(size_t)(k0 + tid) + (size_t)(k0 + j) * n] * yj;
+            }
+            if (tid < kb) y[k0 + tid] = yi;
+        }
+        __syncthreads();
+        const int fend = min(n, (d.tile_last[K] + 1) * kTile);
+        for (int i = k0 + kb + tid; i < fend; i += kFacThreads) {
+            if (d.tile_first[i / kTile] > K) continue;
+            double s = 0.0;
+            for (int p = 0; p < kb; ++p) s += Ad[(size_t)i + (size_t)(k0 + p) * n] * y[k0 + p];
+            y[i] -= s;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += kFacThreads) y[i] = y[i] / Ad[(size_t)i + (size_t)i * n];
+    __syncthreads();
+    // backward: Lᵀ x = y, tile by tile from the bottom
+    for (int K = nt - 1; K >= 0; --K) {
+        const int k0 = K * kTile, kb = min(kTile, n - k0);
+        // y_K -= Σ_{i > tile} L[i][k] y[i]   (column k of L below the tile)
+        const int bend = min(n, (d.tile_last[K] + 1) * kTile);
+        for (int c = tid; c < kb; c += kFacThreads) {
+            double s = 0.0;
+            for (int i = k0 + kb; i < bend; ++i) {
+                if (d.tile_first[i / kTile] > K) continue;
+                s += Ad[(size_t)i + (size_t)(k0 + c) * n] * y[i];
+            }
+            y[k0 + c] -= s;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            double yi = (tid < kb) ? y[k0 + tid] : 0.0;
+            for (int j = kb - 1; j >= 0; --j) {
+                const double yj = __shfl(yi, j, 64);
+                if (tid < j) yi -= Ad[(size_t)(k0 + j) + (size_t)(k0 + tid) * n] * yj;
+            }
+            if (tid < kb) y[k0 + tid] = yi;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += kFacThreads) d.xp[i] = y[i];
+}
+
+// ---------------------------------------------------------------- update + trial evaluation
+__global__ __launch_bounds__(kBlock) void k_pose_update(Dev d) {
+    __shared__ double sh[kBlock / 64];
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    double sc = 0.0;
+    if (k < d.n_kf) {
+        const double *Tc = d.T_cur + (size_t)k * 12;
+        double *Tt = d.T_trial + (size_t)k * 12;
+        const int h = d.kf_hidx[k];
+        if (h >= 0 && d.kf_active[k]) {
+            const double lam = d.ctrl->lambda;
+            double x[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                x[i] = d.xp[6 * h + i];
+                sc += x[i] * (lam * x[i] + d.bp[(size_t)h * 6 + i]);
+            }
+            pose_oplus(Tc, x, Tt);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Tt[i] = Tc[i];
+        }
+    }
+    double s = block_sum<kBlock>(sc, sh);
+    if (threadIdx.x == 0) d.part_ps[blockIdx.x] = s;
+}
+
+template <int DIM>
+__device__ __forceinline__ void landmark_update(const Dev &d, int l, double lam, int solve_ok, double &chi,
+                                                double &sc) {
+    const double *Xc = d.X_cur + (size_t)l * 4;
+    double *Xt = d.X_trial + (size_t)l * 4;
+    double x[4] = {0, 0, 0, 0};
+    if (solve_ok) {
+        double r[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = d.bl[(size_t)l * 4 + i];
+        for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
+            const int h = d.e_hidx[e];
+            if (h < 0) continue;
+            const double *A = d.A + (size_t)e * 12;
+            const double *B = d.B + (size_t)e * 8;
+            double ax0 = 0, ax1 = 0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const double xk = d.xp[6 * h + k];
+                ax0 += A[k] * xk;
+                ax1 += A[6 + k] * xk;
+            }
+#pragma unroll
+            for (int i = 0; i < DIM; ++i) r[i] -= B[i] * ax0 + B[4 + i] * ax1;
+        }
+        double L[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) L[k] = d.Lc[(size_t)l * 10 + k];
+        double y[4];
+#pragma unroll
+        for (int i = 0; i < DIM; ++i) {
+            double t = r[i];
+#pragma unroll
+            for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * y[p];
+            y[i] = t / L[pk(i, i)];
+        }
+#pragma unroll
+        for (int i = DIM - 1; i >= 0; --i) {
+            double t = y[i];
+#pragma unroll
+            for (int p = i + 1; p < DIM; ++p) t -= L[pk(p, i)] * x[p];
+            x[i] = t / L[pk(i, i)];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d.xl[(size_t)l * 4 + i] = x[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = d.xl[(size_t)l * 4 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < DIM; ++i) sc += x[i] * (lam * x[i] + d.bl[(size_t)l * 4 + i]);
+    double X[4];
+    if (DIM == 3) {
+        X[0] = Xc[0] + x[0];
+        X[1] = Xc[1] + x[1];
+        X[2] = Xc[2] + x[2];
+        X[3] = 0.0;
+    } else {
+        double in[4] = {Xc[0], Xc[1], Xc[2], Xc[3]};
+        orth_oplus(in, x, X);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Xt[i] = X[i];
+    double Lp[6];
+    if (DIM == 4) orth_to_pluker(X, Lp);
+    for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
+        if (!d.e_active[e]) continue;
+        const double *T = d.T_trial + (size_t)d.e_kf[e] * 12;
+        const double *obs = d.e_obs + (size_t)e * 4;
+        double err[2];
+        double delta;
+        if (DIM == 3) {
+            double z;
+            point_error(T, X, obs, d.cam, err, z);
+            delta = d.huber_pt;
+        } else {
+            line_error(T, Lp, obs, d.cam, err);
+            delta = d.huber_ln;
+        }
+        const double info = d.e_info[e];
+        const double c2 = err[0] * (info * err[0]) + err[1] * (info * err[1]);
+        d.chi2_last[e] = c2;
+        double rho0 = c2, rho1;
+        if (d.robust) huber(c2, delta, rho0, rho1);
+        chi += rho0;
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_landmark_update(Dev d) {
+    __shared__ double sh[kBlock / 64];
+    const int l = blockIdx.x * kBlock + threadIdx.x;
+    double chi = 0.0, sc = 0.0;
+    if (l < d.n_lm) {
+        if (d.lm_active[l]) {
+            const double lam = d.ctrl->lambda;
+            const int ok = d.ctrl->solve_ok;
+            if (is_point_lm(d, l)) landmark_update<3>(d, l, lam, ok, chi, sc);
+            else landmark_update<4>(d, l, lam, ok, chi, sc);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d.X_trial[(size_t)l * 4 + i] = d.X_cur[(size_t)l * 4 + i];
+        }
+    }
+    double s1 = block_sum<kBlock>(chi, sh);
+    double s2 = block_sum<kBlock>(sc, sh);
+    if (threadIdx.x == 0) {
+        d.part_lm[blockIdx.x] = s1;
+        d.part_lms[blockIdx.x] = s2;
+    }
+}
+
+// OptimizationAlgorithmLevenberg trial decision
+__global__ __launch_bounds__(kBlock) void k_decide(Dev d, int max_trials) {
+    __shared__ double sh[kBlock / 64];
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) { a += d.part_lm[i]; b += d.part_lms[i]; }
+    for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];
+    const double tempChi0 = block_sum<kBlock>(a, sh);
+    const double scale0 = block_sum<kBlock>(b, sh);
+    if (threadIdx.x == 0) {
+        Ctrl *c = d.ctrl;
+        double tempChi = tempChi0;
+        if (!c->solve_ok) tempChi = 1.7976931348623157e308;
+        const double scale = scale0 + 1e-3;
+        const double rho = (c->currentChi - tempChi) / scale;
+        c->tempChi = tempChi;
+        c->scale = scale;
+        c->rho = rho;
+        if (rho > 0 && isfinite(tempChi)) {
+            double alpha = 1. - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2. / 3.);
+            const double sf = fmax(1. / 3., alpha);
+            c->lambda *= sf;
+            c->ni = 2;
+            c->currentChi = tempChi;
+            c->accept = 1;
+            c->qmax += 1;
+        } else {
+            c->lambda *= c->ni;
+            c->ni *= 2;
+            c->accept = 0;
+            if (!isfinite(c->lambda)) c->broke = 1;
+            else c->qmax += 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_commit(Dev d) {
+    if (!d.ctrl->accept) return;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < d.n_kf && d.kf_hidx[i] >= 0 && d.kf_active[i]) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) d.T_cur[(size_t)i * 12 + k] = d.T_trial[(size_t)i * 12 + k];
+    }
+    if (i < d.n_lm && d.lm_active[i]) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d.X_cur[(size_t)i * 4 + k] = d.X_trial[(size_t)i * 4 + k];
+    }
+}
+
+// ---------------------------------------------------------------- outlier pass helpers
+// classification after stage 1 (src/mapHandler.cpp:6125-6147): level |= bad
+__global__ void k_classify(Dev d, double thr) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= d.E) return;
+    bool bad = d.chi2_last[e] > thr;
+    if (e < d.Ep) {
+        double Pc[3];
+        point_pc(d.T_cur + (size_t)d.e_kf[e] * 12, d.X_cur + (size_t)d.e_lm[e] * 4, Pc);
+        bad = bad || !(Pc[2] > 0.0);
+    }
+    if (bad) d.e_level[e] = 1;
+}
+// computeError() at the current state for edges of `level`
+__global__ void k_refresh(Dev d, int level) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= d.E || d.e_level[e] != level) return;
+    const double *T = d.T_cur + (size_t)d.e_kf[e] * 12;
+    const double *X = d.X_cur + (size_t)d.e_lm[e] * 4;
+    const double *obs = d.e_obs + (size_t)e * 4;
+    double err[2];
+    if (e < d.Ep) {
+        double z;
+        point_error(T, X, obs, d.cam, err, z);
+    } else {
+        double L[6];
+        orth_to_pluker(X, L);
+        line_error(T, L, obs, d.cam, err);
+    }
+    const double info = d.e_info[e];
+    d.chi2_last[e] = err[0] * (info * err[0]) + err[1] * (info * err[1]);
+}
+// isDepthPositive() at the current state
+__global__ void k_depth(Dev d, uint8_t *out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= d.Ep) return;
+    double Pc[3];
+    point_pc(d.T_cur + (size_t)d.e_kf[e] * 12, d.X_cur + (size_t)d.e_lm[e] * 4, Pc);
+    out[e] = Pc[2] > 0.0 ? 1 : 0;
+}
+
+}  // namespace plba

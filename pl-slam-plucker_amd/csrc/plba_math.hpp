@@ -1,0 +1,272 @@
+// plba_math.hpp — device restatement of the g2o_types vertex/edge arithmetic (FP64).
+//
+// Every function follows the reference formula order so that the GPU path rounds like the
+// reference does wherever the data flow allows:
+//   vechat                      g2o_types/g2o_types.h:18-24
+//   pose oplus (quaternion)     g2o_types/g2o_types.h:172-203  (+ Eigen toRotationMatrix)
+//   orth oplus (updateOrthCoord)g2o_types/g2o_types.h:72-130
+//   point reprojection error    g2o_types/g2o_types.h:224-263
+//   point Jacobians             g2o_types/g2o_types.h:271-296
+//   line error (Plücker)        g2o_types/g2o_types.h:320-387
+//   line Jacobians              g2o_types/g2o_types.h:389-495 (incl. the orth-as-Plücker pose
+//                               block of :429-430 unless `corrected`)
+//   Huber robustify             g2o RobustKernelHuber
+// Poses are Tcw stored row-major 3x4 [R | t] (12 doubles).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#define PLBA_HD __host__ __device__ __forceinline__
+
+namespace plba {
+
+struct Cam {
+    double fx, fy, cx, cy;
+};
+
+PLBA_HD void mat3vec(const double *R, const double *v, double *r) {
+    r[0] = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    r[1] = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    r[2] = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+}
+PLBA_HD void mat3mul(const double *A, const double *B, double *C) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[i * 3 + j] = A[i * 3 + 0] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
+}
+PLBA_HD void vechat(const double *v, double *M) {
+    M[0] = 0;     M[1] = -v[2]; M[2] = v[1];
+    M[3] = v[2];  M[4] = 0;     M[5] = -v[0];
+    M[6] = -v[1]; M[7] = v[0];  M[8] = 0;
+}
+PLBA_HD void rot_xyz(const double *th, double *R) {
+    double s1 = sin(th[0]), c1 = cos(th[0]);
+    double s2 = sin(th[1]), c2 = cos(th[1]);
+    double s3 = sin(th[2]), c3 = cos(th[2]);
+    R[0] = c2 * c3; R[1] = s1 * s2 * c3 - c1 * s3; R[2] = c1 * s2 * c3 + s1 * s3;
+    R[3] = c2 * s3; R[4] = s1 * s2 * s3 + c1 * c3; R[5] = c1 * s2 * s3 - s1 * c3;
+    R[6] = -s2;     R[7] = s1 * c2;                R[8] = c1 * c2;
+}
+// changeOrthToPluker (g2o_types.h:367-387)
+PLBA_HD void orth_to_pluker(const double *o, double *L) {
+    double R[9];
+    rot_xyz(o, R);
+    double w1 = cos(o[3]), w2 = sin(o[3]);
+    L[0] = w1 * R[0]; L[1] = w1 * R[3]; L[2] = w1 * R[6];
+    L[3] = w2 * R[1]; L[4] = w2 * R[4]; L[5] = w2 * R[7];
+}
+
+// VertexLMPose::oplusImpl — R <- R(q)·R, t <- t + δt (δ = [δt; δω])
+PLBA_HD void pose_oplus(const double *Tin, const double *d, double *Tout) {
+    const double wx = d[3], wy = d[4], wz = d[5];
+    double theta = sqrt(wx * wx + wy * wy + wz * wz);
+    double half = 0.5 * theta;
+    double imag, real = cos(half);
+    if (theta < 1e-10) {
+        double tsq = theta * theta, t4 = tsq * tsq;
+        imag = 0.5 - 0.0208333 * tsq + 0.000260417 * t4;
+    } else {
+        imag = sin(half) / theta;
+    }
+    double qw = real, qx = imag * wx, qy = imag * wy, qz = imag * wz;
+    double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
+    double twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    double txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    double dR[9] = {1 - (tyy + tzz), txy - twz,       txz + twy,
+                    txy + twz,       1 - (txx + tzz), tyz - twx,
+                    txz - twy,       tyz + twx,       1 - (txx + tyy)};
+    double R[9] = {Tin[0], Tin[1], Tin[2], Tin[4], Tin[5], Tin[6], Tin[8], Tin[9], Tin[10]};
+    double Rn[9];
+    mat3mul(dR, R, Rn);
+    Tout[0] = Rn[0]; Tout[1] = Rn[1]; Tout[2] = Rn[2];  Tout[3] = Tin[3] + d[0];
+    Tout[4] = Rn[3]; Tout[5] = Rn[4]; Tout[6] = Rn[5];  Tout[7] = Tin[7] + d[1];
+    Tout[8] = Rn[6]; Tout[9] = Rn[7]; Tout[10] = Rn[8]; Tout[11] = Tin[11] + d[2];
+}
+
+// VertexLMLineOrth::updateOrthCoord
+PLBA_HD void orth_oplus(const double *D, const double *dD, double *out) {
+    double R[9];
+    rot_xyz(D, R);
+    double w1 = cos(D[3]), w2 = sin(D[3]);
+    double cz = cos(dD[2]), sz = sin(dD[2]);
+    double cy = cos(dD[1]), sy = sin(dD[1]);
+    double cx = cos(dD[0]), sx = sin(dD[0]);
+    const double Rz[9] = {cz, -sz, 0, sz, cz, 0, 0, 0, 1};
+    const double Ry[9] = {cy, 0, sy, 0, 1, 0, -sy, 0, cy};
+    const double Rx[9] = {1, 0, 0, 0, cx, -sx, 0, sx, cx};
+    double T1[9], T2[9], Rn[9];
+    mat3mul(R, Rx, T1);
+    mat3mul(T1, Ry, T2);
+    mat3mul(T2, Rz, Rn);
+    double cp = cos(dD[3]), sp = sin(dD[3]);
+    double W10 = w2 * cp + w1 * sp;
+    out[0] = atan2(Rn[7], Rn[8]);
+    out[1] = asin(-Rn[6]);
+    out[2] = atan2(Rn[3], Rn[0]);
+    out[3] = asin(W10);
+}
+
+// RobustKernelHuber::robustify -> rho0, rho1
+PLBA_HD void huber(double e, double delta, double &rho0, double &rho1) {
+    double dsqr = delta * delta;
+    if (e <= dsqr) {
+        rho0 = e;
+        rho1 = 1.0;
+    } else {
+        double sqrte = sqrt(e);
+        rho0 = 2 * sqrte * delta - dsqr;
+        rho1 = delta / sqrte;
+    }
+}
+
+// ---------------- EdgePosePoint ----------------
+PLBA_HD void point_pc(const double *T, const double *P, double *Pc) {
+    Pc[0] = T[0] * P[0] + T[1] * P[1] + T[2] * P[2] + T[3];
+    Pc[1] = T[4] * P[0] + T[5] * P[1] + T[6] * P[2] + T[7];
+    Pc[2] = T[8] * P[0] + T[9] * P[1] + T[10] * P[2] + T[11];
+}
+PLBA_HD void point_error(const double *T, const double *P, const double *obs, const Cam &c, double *e, double &z) {
+    double Pc[3];
+    point_pc(T, P, Pc);
+    double u = (Pc[0] / Pc[2]) * c.fx + c.cx;
+    double v = (Pc[1] / Pc[2]) * c.fy + c.cy;
+    e[0] = obs[0] - u;
+    e[1] = obs[1] - v;
+    z = Pc[2];
+}
+// Jl: 2x3 (row-major), Jp: 2x6
+PLBA_HD void point_jac(const double *T, const double *P, const Cam &c, double *Jl, double *Jp) {
+    double Pc[3];
+    point_pc(T, P, Pc);
+    double x = Pc[0], y = Pc[1], z = Pc[2];
+    double invz = 1.0 / z, invz2 = invz * invz;
+    const double J[6] = {c.fx / z, 0, -c.fx * x * invz2, 0, c.fy / z, -c.fy * y * invz2};
+    const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            Jl[r * 3 + k] = -(J[r * 3 + 0] * R[k] + J[r * 3 + 1] * R[3 + k] + J[r * 3 + 2] * R[6 + k]);
+    double RP[3], S[9];
+    mat3vec(R, P, RP);
+    vechat(RP, S);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) Jp[r * 6 + k] = -J[r * 3 + k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            Jp[r * 6 + 3 + k] = -(J[r * 3 + 0] * (-S[k]) + J[r * 3 + 1] * (-S[3 + k]) + J[r * 3 + 2] * (-S[6 + k]));
+    }
+}
+
+// ---------------- EdgePoseLine ----------------
+// l = K_L * (R n + [t]x R d)
+PLBA_HD void line_image(const double *T, const double *L, const Cam &c, double *l) {
+    const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+    const double t[3] = {T[3], T[7], T[11]};
+    double Rn[3], Rd[3], S[9], tRd[3];
+    mat3vec(R, L, Rn);
+    mat3vec(R, L + 3, Rd);
+    vechat(t, S);
+    mat3vec(S, Rd, tRd);
+    double nc0 = Rn[0] + tRd[0], nc1 = Rn[1] + tRd[1], nc2 = Rn[2] + tRd[2];
+    l[0] = c.fy * nc0;
+    l[1] = c.fx * nc1;
+    l[2] = (-c.fy * c.cx) * nc0 + (-c.fx * c.cy) * nc1 + (c.fx * c.fy) * nc2;
+}
+PLBA_HD void line_error(const double *T, const double *L, const double *obs, const Cam &c, double *e) {
+    double l[3];
+    line_image(T, L, c, l);
+    double f = sqrt(l[0] * l[0] + l[1] * l[1]);
+    e[0] = (l[0] * obs[0] + l[1] * obs[1] + l[2]) / f;
+    e[1] = (l[0] * obs[2] + l[1] * obs[3] + l[2]) / f;
+}
+// Jl: 2x4 (row-major), Jp: 2x6 ; also returns the error
+PLBA_HD void line_jac(const double *T, const double *orth, const double *L, const double *obs, const Cam &c,
+                      int corrected, double *e, double *Jl, double *Jp) {
+    const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+    const double t[3] = {T[3], T[7], T[11]};
+    double l[3];
+    line_image(T, L, c, l);
+    double lx = l[0], ly = l[1], lz = l[2];
+    double f = sqrt(lx * lx + ly * ly);
+    double e0 = (lx * obs[0] + ly * obs[1] + lz) / f;
+    double e1 = (lx * obs[2] + ly * obs[3] + lz) / f;
+    e[0] = e0;
+    e[1] = e1;
+    const double j[2][3] = {{-lx * e0 / (f * f) + obs[0] / f, -ly * e0 / (f * f) + obs[1] / f, 1.0 / f},
+                            {-lx * e1 / (f * f) + obs[2] / f, -ly * e1 / (f * f) + obs[3] / f, 1.0 / f}};
+    const double K[9] = {c.fy, 0, 0, 0, c.fx, 0, -c.fy * c.cx, -c.fx * c.cy, c.fx * c.fy};
+    double jK[2][3];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) jK[r][k] = j[r][0] * K[k] + j[r][1] * K[3 + k] + j[r][2] * K[6 + k];
+    double a[3], b[3];
+    if (!corrected) {  // Lw.tail(3) / Lw.head(3) of the 4-vector orth estimate (g2o_types.h:429-430)
+        a[0] = orth[1]; a[1] = orth[2]; a[2] = orth[3];
+        b[0] = orth[0]; b[1] = orth[1]; b[2] = orth[2];
+    } else {
+        a[0] = L[3]; a[1] = L[4]; a[2] = L[5];
+        b[0] = L[0]; b[1] = L[1]; b[2] = L[2];
+    }
+    double Ra[3], Rb[3], Sa[9], Sb[9], St[9], StSa[9];
+    mat3vec(R, a, Ra);
+    mat3vec(R, b, Rb);
+    vechat(Ra, Sa);
+    vechat(Rb, Sb);
+    vechat(t, St);
+    mat3mul(St, Sa, StSa);
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            Jp[r * 6 + k] = jK[r][0] * (-Sa[k]) + jK[r][1] * (-Sa[3 + k]) + jK[r][2] * (-Sa[6 + k]);
+            Jp[r * 6 + 3 + k] = jK[r][0] * (-Sb[k] - StSa[k]) + jK[r][1] * (-Sb[3 + k] - StSa[3 + k]) +
+                                jK[r][2] * (-Sb[6 + k] - StSa[6 + k]);
+        }
+    // U, W recomputed from the Plücker vector (getOrhtRFromPluker / getOrthWFromPluker)
+    double nn = sqrt(L[0] * L[0] + L[1] * L[1] + L[2] * L[2]);
+    double dn = sqrt(L[3] * L[3] + L[4] * L[4] + L[5] * L[5]);
+    double cr[3] = {L[1] * L[5] - L[2] * L[4], L[2] * L[3] - L[0] * L[5], L[0] * L[4] - L[1] * L[3]};
+    double cn = sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+    double fw = sqrt(nn * nn + dn * dn);
+    double w1 = nn / fw, w2 = dn / fw;
+    double u1[3], u2[3], u3[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        u1[i] = L[i] / nn;
+        u2[i] = L[3 + i] / dn;
+        u3[i] = cr[i] / cn;
+    }
+    double StR[9];
+    mat3mul(St, R, StR);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        double v[6];  // jK * [R | [t]x R]
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v[k] = jK[r][0] * R[k] + jK[r][1] * R[3 + k] + jK[r][2] * R[6 + k];
+            v[3 + k] = jK[r][0] * StR[k] + jK[r][1] * StR[3 + k] + jK[r][2] * StR[6 + k];
+        }
+        // jacobianFromPlukerToOrth columns
+        double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s0 += v[3 + i] * (w2 * u3[i]);
+            s1 += v[i] * (-w1 * u3[i]);
+            s2 += v[i] * (w1 * u2[i]) + v[3 + i] * (-w2 * u1[i]);
+            s3 += v[i] * (-w2 * u1[i]) + v[3 + i] * (w1 * u2[i]);
+        }
+        Jl[r * 4 + 0] = s0;
+        Jl[r * 4 + 1] = s1;
+        Jl[r * 4 + 2] = s2;
+        Jl[r * 4 + 3] = s3;
+    }
+}
+
+}  // namespace plba

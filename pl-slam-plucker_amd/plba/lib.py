@@ -1,0 +1,197 @@
+"""ctypes binding of libplba.so (the HIP backend, C ABI of include/plba.h).
+
+This is the product path: it fails loudly when the HIP library is missing or no GPU is
+visible — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import capi
+from .synth import Graph
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libplba.so")
+
+_lib = None
+
+PLBA_ERRORS = {-1: "PLBA_E_INVALID", -2: "PLBA_E_DEVICE", -3: "PLBA_E_STATE", -4: "PLBA_E_NOMEM", -5: "PLBA_E_COMM"}
+
+EXPORTED = [
+    "plba_default_opts", "plba_create", "plba_destroy", "plba_last_error", "plba_upload", "plba_reset_estimates",
+    "plba_set_edge_levels", "plba_set_robust", "plba_initialize_optimization", "plba_optimize",
+    "plba_refresh_edge_errors", "plba_get_edge_chi2", "plba_download", "plba_lba_plucker", "plba_get_trace",
+    "plba_synchronize", "plba_enable_kernel_timing", "plba_kernel_times",
+]
+
+
+class PlbaError(RuntimeError):
+    pass
+
+
+def load(path: Optional[str] = None):
+    """Load libplba.so (raises if it is missing — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise PlbaError(f"libplba.so not found at {path}: run `make -C pl-slam-plucker_amd` "
+                        "(or __graft_entry__.build()) first")
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    dp = C.POINTER(C.c_double)
+    bp = C.POINTER(C.c_uint8)
+    ip = C.POINTER(C.c_int32)
+    L.plba_default_opts.argtypes = [C.POINTER(capi.PlbaOpts)]
+    L.plba_default_opts.restype = None
+    L.plba_create.argtypes = [C.POINTER(vp), C.POINTER(capi.PlbaOpts)]
+    L.plba_destroy.argtypes = [vp]
+    L.plba_last_error.argtypes = [vp]
+    L.plba_last_error.restype = C.c_char_p
+    L.plba_upload.argtypes = [vp, C.POINTER(capi.PlbaGraph)]
+    L.plba_reset_estimates.argtypes = [vp]
+    L.plba_set_edge_levels.argtypes = [vp, bp, bp]
+    L.plba_set_robust.argtypes = [vp, C.c_int32]
+    L.plba_initialize_optimization.argtypes = [vp, C.c_int32]
+    L.plba_optimize.argtypes = [vp, C.c_int32, ip, dp]
+    L.plba_refresh_edge_errors.argtypes = [vp, C.c_int32]
+    L.plba_get_edge_chi2.argtypes = [vp, dp, bp, dp]
+    L.plba_download.argtypes = [vp, dp, dp, dp]
+    L.plba_lba_plucker.argtypes = [vp, C.POINTER(capi.PlbaResult)]
+    L.plba_get_trace.argtypes = [vp, C.POINTER(capi.PlbaIterTrace), C.c_int32, ip]
+    L.plba_synchronize.argtypes = [vp]
+    L.plba_enable_kernel_timing.argtypes = [vp, C.c_int32]
+    L.plba_kernel_times.argtypes = [vp, C.POINTER(C.c_char_p), dp, ip, C.c_int32, ip]
+    for name in EXPORTED:
+        f = getattr(L, name)
+        if name not in ("plba_default_opts", "plba_last_error"):
+            f.restype = C.c_int
+    _lib = L
+    return L
+
+
+def _p(a, t=C.c_double):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class Solver:
+    """One plba context bound to a device (g2o::SparseOptimizer equivalent)."""
+
+    def __init__(self, device: int = 0, corrected_line_jacobian: bool = False, verbose: bool = False,
+                 kernel_timing: bool = False):
+        self.L = load()
+        o = capi.PlbaOpts()
+        self.L.plba_default_opts(C.byref(o))
+        o.device = device
+        o.corrected_line_jacobian = int(corrected_line_jacobian)
+        o.verbose = int(verbose)
+        self.ctx = C.c_void_p()
+        rc = self.L.plba_create(C.byref(self.ctx), C.byref(o))
+        if rc != 0:
+            raise PlbaError(f"plba_create failed: {PLBA_ERRORS.get(rc, rc)} (no usable HIP device?)")
+        self.graph: Optional[Graph] = None
+        if kernel_timing:
+            self._check(self.L.plba_enable_kernel_timing(self.ctx, 1), "plba_enable_kernel_timing")
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.L.plba_last_error(self.ctx).decode(errors="replace")
+            raise PlbaError(f"{what} failed: {PLBA_ERRORS.get(rc, rc)}: {msg}")
+
+    def close(self):
+        if self.ctx:
+            self.L.plba_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- g2o-style calls
+    def upload(self, g: Graph):
+        self.graph = g
+        gv = capi.GraphView(g)
+        self._check(self.L.plba_upload(self.ctx, C.byref(gv.struct)), "plba_upload")
+
+    def reset(self):
+        self._check(self.L.plba_reset_estimates(self.ctx), "plba_reset_estimates")
+
+    def set_edge_levels(self, ept_level, eln_level):
+        a = np.ascontiguousarray(ept_level, np.uint8)
+        b = np.ascontiguousarray(eln_level, np.uint8)
+        self._check(self.L.plba_set_edge_levels(self.ctx, _p(a, C.c_uint8), _p(b, C.c_uint8)), "plba_set_edge_levels")
+
+    def set_robust(self, on: bool):
+        self._check(self.L.plba_set_robust(self.ctx, int(on)), "plba_set_robust")
+
+    def initialize_optimization(self, level: int = 0):
+        self._check(self.L.plba_initialize_optimization(self.ctx, level), "plba_initialize_optimization")
+
+    def optimize(self, iterations: int):
+        it = C.c_int32(0)
+        chi = C.c_double(0)
+        self._check(self.L.plba_optimize(self.ctx, iterations, C.byref(it), C.byref(chi)), "plba_optimize")
+        return it.value, chi.value
+
+    def refresh_edge_errors(self, level: int):
+        self._check(self.L.plba_refresh_edge_errors(self.ctx, level), "plba_refresh_edge_errors")
+
+    def edge_chi2(self):
+        g = self.graph
+        pc, pd, lc = np.zeros(g.n_ept), np.zeros(g.n_ept, np.uint8), np.zeros(g.n_eln)
+        self._check(self.L.plba_get_edge_chi2(self.ctx, _p(pc), _p(pd, C.c_uint8), _p(lc)), "plba_get_edge_chi2")
+        return pc, pd, lc
+
+    def download(self):
+        g = self.graph
+        T, P, O = np.zeros((g.n_kf, 3, 4)), np.zeros((g.n_pt, 3)), np.zeros((g.n_ln, 4))
+        self._check(self.L.plba_download(self.ctx, _p(T), _p(P), _p(O)), "plba_download")
+        return T, P, O
+
+    def lba_plucker(self, want_outputs: bool = True) -> dict:
+        """Full two-stage schedule (src/mapHandler.cpp:6119-6160) on the uploaded window."""
+        g = self.graph
+        if want_outputs:
+            rb = capi.ResultBuffers(g)
+            self._check(self.L.plba_lba_plucker(self.ctx, C.byref(rb.struct)), "plba_lba_plucker")
+            out = rb.as_dict()
+        else:
+            r = capi.PlbaResult()
+            self._check(self.L.plba_lba_plucker(self.ctx, C.byref(r)), "plba_lba_plucker")
+            out = dict(iters=np.array([r.iters[0], r.iters[1]]), chi2=np.array([r.chi2[0], r.chi2[1]]),
+                       solve_ms=r.solve_ms)
+        out["trace"] = self.trace()
+        return out
+
+    def trace(self) -> np.ndarray:
+        n = C.c_int32(0)
+        self._check(self.L.plba_get_trace(self.ctx, None, 0, C.byref(n)), "plba_get_trace")
+        buf = (capi.PlbaIterTrace * max(n.value, 1))()
+        self._check(self.L.plba_get_trace(self.ctx, buf, n.value, C.byref(n)), "plba_get_trace")
+        return capi.trace_to_array(buf, n.value)
+
+    def kernel_times(self) -> dict:
+        cap = 32
+        names = (C.c_char_p * cap)()
+        ms = np.zeros(cap)
+        nl = np.zeros(cap, np.int32)
+        n = C.c_int32(0)
+        self._check(self.L.plba_kernel_times(self.ctx, names, _p(ms), _p(nl, C.c_int32), cap, C.byref(n)),
+                    "plba_kernel_times")
+        return {names[i].decode(): (float(ms[i]), int(nl[i])) for i in range(n.value)}
+
+    def synchronize(self):
+        self._check(self.L.plba_synchronize(self.ctx), "plba_synchronize")
