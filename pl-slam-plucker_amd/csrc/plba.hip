@@ -58,6 +58,7 @@ struct plba_ctx {
     // device arena
     std::vector<void *> allocs;
     Ctrl *h_ctrl = nullptr;  // pinned
+    uint8_t *d_depth = nullptr;  // [Ep] isDepthPositive flags
     // host-side bookkeeping
     int32_t n_kf = 0, n_pt = 0, n_ln = 0, Ep = 0, El = 0;
     std::vector<int32_t> e_orig;        // CSR edge -> original index within its type
@@ -113,6 +114,10 @@ struct plba_ctx {
 namespace {
 
 inline int blocks_for(int n, int b = kBlock) { return (n + b - 1) / b; }
+inline size_t band_lds_bytes(int bw) {
+    const size_t W = bw + 1;
+    return sizeof(double) * (W * W * 36 + W * 6 + W * 36 + 36 + W * 6 + W * 6 + 6);
+}
 
 // time a launch when kernel timing is enabled
 template <typename F>
@@ -274,6 +279,24 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
                 blk_trip[bi].push_back({a, b});
             }
     }
+    // envelope (first block column per block row) and bandwidth
+    std::vector<int32_t> first_blk(nf);
+    for (int h = 0; h < nf; ++h) first_blk[h] = h;
+    for (auto &bk : blocks) first_blk[bk.second] = std::min(first_blk[bk.second], bk.first);
+    int bw = 0;
+    for (int h = 0; h < nf; ++h) bw = std::max(bw, h - first_blk[h]);
+    const bool band_mode = bw <= kBandMax;
+    if (band_mode) {  // every envelope block is written each trial (zeros where no landmark couples)
+        for (int i2 = 0; i2 < nf; ++i2)
+            for (int i1 = first_blk[i2]; i1 < i2; ++i1) {
+                auto key = std::make_pair(i1, i2);
+                if (!blk_index.count(key)) {
+                    blk_index[key] = (int)blocks.size();
+                    blocks.push_back(key);
+                    blk_trip.emplace_back();
+                }
+            }
+    }
     const int nblk = (int)blocks.size();
     std::vector<int32_t> blk_i1(nblk), blk_i2(nblk), blk_off(nblk + 1, 0), trip;
     {
@@ -299,9 +322,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // envelope of the lower triangle (per 6-row pose block: first pose block column)
     const int n = 6 * nf;
     const int ntiles = (n + kTile - 1) / kTile;
-    std::vector<int32_t> first_blk(nf);
-    for (int h = 0; h < nf; ++h) first_blk[h] = h;
-    for (int k = 0; k < nblk; ++k) first_blk[blk_i2[k]] = std::min(first_blk[blk_i2[k]], blk_i1[k]);
     std::vector<int32_t> tile_first(std::max(ntiles, 1), 0), tile_last(std::max(ntiles, 1), 0);
     for (int I = 0; I < ntiles; ++I) {
         int f = I;
@@ -319,6 +339,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     Dev &d = ctx->d;
     d.n_kf = n_kf; d.n_pt = n_pt; d.n_ln = n_ln; d.n_lm = n_lm; d.Ep = Ep; d.El = El; d.E = E;
     d.nf = nf; d.n = n; d.nblk = nblk; d.ntiles = ntiles;
+    d.bw = bw;
+    d.band_mode = band_mode ? 1 : 0;
     d.corrected = ctx->opts.corrected_line_jacobian;
     d.robust = 1;
     d.cam = Cam{g->fx, g->fy, g->cx, g->cy};
@@ -379,7 +401,12 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.blk_i2, blk_i2);
     UPLOAD(d.blk_off, blk_off);
     UPLOAD(d.trip, trip);
-    ALLOC(d.Ad, (size_t)n * n);
+    ALLOC(d.Ad, band_mode ? 1 : (size_t)n * n);
+    UPLOAD(d.first_blk, first_blk);
+    ALLOC(d.Bd, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
+    ALLOC(d.Lband, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
+    ALLOC(d.Kinv, (size_t)nf * 36);
+    ALLOC(d.zb, (size_t)nf * 6);
     ALLOC(d.bs, n);
     ALLOC(d.xp, n);
     ALLOC(d.Wbuf, (size_t)std::max(n, 1) * kTile);
@@ -391,8 +418,15 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_lms, d.n_lm_blocks);
     ALLOC(d.part_ps, d.n_kf_blocks);
     ALLOC(d.ctrl, 1);
+    ALLOC(ctx->d_depth, Ep);
 #undef ALLOC
 #undef UPLOAD
+    if (band_mode) {
+        PLBA_CHECK(hipFuncSetAttribute((const void *)k_rcs_factor_band<256>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_lds_bytes(bw)));
+        PLBA_CHECK(hipFuncSetAttribute((const void *)k_rcs_factor_band<1024>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_lds_bytes(bw)));
+    }
     PLBA_CHECK(hipMemset(d.e_level, 0, E));
     PLBA_CHECK(hipMemset(d.xp, 0, sizeof(double) * std::max(n, 1)));
     PLBA_CHECK(hipMemset(d.xl, 0, sizeof(double) * std::max(n_lm, 1) * 4));
@@ -435,9 +469,15 @@ int lm_iteration(plba_ctx *ctx, int it) {
     for (;;) {
         if (d.n_lm > 0) LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_schur_landmark, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
         if (d.n > 0) {
-            LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
+            if (!d.band_mode)
+                LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
             LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_assemble, dim3(blocks_for(d.nblk * 64)), dim3(kBlock), 0, s, d));
-            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
+            if (d.band_mode && d.bw <= 8)
+                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor_band<256>, dim3(1), dim3(256), band_lds_bytes(d.bw), s, d));
+            else if (d.band_mode)
+                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor_band<1024>, dim3(1), dim3(1024), band_lds_bytes(d.bw), s, d));
+            else
+                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
         } else {
             int one = 1;
             PLBA_CHECK(hipMemcpyAsync(&d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, s));
@@ -625,13 +665,10 @@ int plba_get_edge_chi2(plba_ctx *ctx, double *ept_chi2, uint8_t *ept_depth_ok, d
     Dev &d = ctx->d;
     std::vector<double> chi(d.E);
     std::vector<uint8_t> dep(d.Ep);
-    uint8_t *ddep = nullptr;
     if (ept_depth_ok && d.Ep) {
-        PLBA_CHECK(hipMallocAsync((void **)&ddep, d.Ep, ctx->stream));
-        hipLaunchKernelGGL(k_depth, dim3(blocks_for(d.Ep)), dim3(kBlock), 0, ctx->stream, d, ddep);
+        hipLaunchKernelGGL(k_depth, dim3(blocks_for(d.Ep)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth);
         PLBA_CHECK(hipGetLastError());
-        PLBA_CHECK(hipMemcpyAsync(dep.data(), ddep, d.Ep, hipMemcpyDeviceToHost, ctx->stream));
-        PLBA_CHECK(hipFreeAsync(ddep, ctx->stream));
+        PLBA_CHECK(hipMemcpyAsync(dep.data(), ctx->d_depth, d.Ep, hipMemcpyDeviceToHost, ctx->stream));
     }
     if (d.E) PLBA_CHECK(hipMemcpyAsync(chi.data(), d.chi2_last, sizeof(double) * d.E, hipMemcpyDeviceToHost, ctx->stream));
     PLBA_CHECK(hipStreamSynchronize(ctx->stream));

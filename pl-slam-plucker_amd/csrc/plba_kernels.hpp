@@ -25,7 +25,8 @@
 namespace plba {
 
 constexpr int kBlock = 256;
-constexpr int kTile = 32;   // RCS factorisation tile
+constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
+constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window factorisation holds
 
 struct Ctrl {
     double lambda, ni, currentChi, tempChi, rho, scale, maxdiag;
@@ -65,6 +66,13 @@ struct Dev {
     double *Ad, *bs, *xp, *Wbuf;        // [n*n], [n], [n], [n*kTile]
     int32_t *tile_first;                // [ntiles] first nonzero column tile of each row tile
     int32_t *tile_last;                 // [ntiles] last row tile whose envelope reaches column tile K
+    // block-band storage (used when the envelope bandwidth bw <= kBandMax)
+    int32_t bw, band_mode;              // bandwidth in pose blocks; 1 = banded factorisation
+    int32_t *first_blk;                 // [nf] first block column of each block row (lower)
+    double *Bd;                         // [nf][bw+1][36]  block (i, i-w), row-major 6x6
+    double *Lband;                      // [nf][bw+1][36]  L_{i,i-w} (w >= 1)
+    double *Kinv;                       // [nf][36]        S_k^{-1}
+    double *zb;                         // [nf][6]         z = D_B^{-1} y
     // reductions
     double *part_chi2;                  // [n_lin_blocks]
     double *part_max;                   // [nf + n_lm_blocks]
@@ -433,7 +441,8 @@ __global__ __launch_bounds__(kBlock) void k_rcs_assemble(Dev d) {
             for (int k = 0; k < 36; ++k) v = (k == lane) ? acc[k] : v;
             double h = d.Hpp[(size_t)i1 * 36 + lane] - v;
             if (r == c) h += lam;
-            d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
+            if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + lane] = h;
+            else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
         }
         if (lane < 6) {
             double v = 0.0;
@@ -447,7 +456,8 @@ __global__ __launch_bounds__(kBlock) void k_rcs_assemble(Dev d) {
 #pragma unroll
         for (int k = 0; k < 36; ++k) v = (k == lane) ? acc[k] : v;
         // block (i1,i2) row r of i1, col c of i2  -> lower position (6 i2 + c, 6 i1 + r)
-        d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -v;
+        if (d.band_mode) d.Bd[((size_t)i2 * (d.bw + 1) + (i2 - i1)) * 36 + c * 6 + r] = -v;
+        else d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -v;
     }
 }
 
@@ -592,6 +602,182 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
         __syncthreads();
     }
     for (int i = tid; i < n; i += kFacThreads) d.xp[i] = y[i];
+}
+
+
+// Block-banded LDLᵀ of the reduced camera system (A = L_B D_B L_Bᵀ, 6x6 pose blocks) with an
+// LDS sliding window of bw+1 block rows, forward substitution folded in (augmented column b),
+// then a one-wave backward pass. One workgroup; 3 barriers per pose block.
+// Failure semantics of SimplicialLDLT: a zero pivot (Gauss–Jordan pivots of S_k are the LDLᵀ
+// pivots) fails the solve and x_p keeps its previous value.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rcs_factor_band(Dev d) {
+    extern __shared__ double lds[];
+    const int bw = d.bw, W = bw + 1, nf = d.nf;
+    double *win = lds;                          // [W slots][W][36]
+    double *bwin = win + (size_t)W * W * 36;    // [W][6]
+    double *Lcol = bwin + (size_t)W * 6;        // [W][36]  (index w = 1..bw)
+    double *Kv = Lcol + (size_t)W * 36;         // [36]
+    double *xr = Kv + 36;                       // [W][6]  ring of solved x blocks
+    double *part = xr + (size_t)W * 6;          // [W][6]
+    double *yk = part + (size_t)W * 6;          // [6]  y_k snapshot (slot sk is refilled in phase C)
+    __shared__ int s_fail;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_fail = 0;
+    // initial window: rows 0..min(bw, nf-1)
+    for (int t = tid; t < W * W * 36; t += NT) {
+        const int row = t / (W * 36), rem = t % (W * 36);
+        win[t] = (row < nf) ? d.Bd[((size_t)row * W) * 36 + rem] : 0.0;
+    }
+    for (int t = tid; t < W * 6; t += NT) bwin[t] = (t / 6 < nf) ? d.bs[t] : 0.0;
+    // refill prefetch registers: thread t owns entries t, t+NT, ... of one W*36 block row (+6 of b)
+    constexpr int kMaxPf = (kBandMax + 1) * 36 / NT + 1;
+    double pf[kMaxPf];
+    double pfb = 0.0;
+    __syncthreads();
+    for (int k = 0; k < nf; ++k) {
+        const int sk = k % W;
+        {   // issue the loads of block row k+W now; they land in LDS in phase C
+            const int inew = k + W;
+#pragma unroll
+            for (int q = 0; q < kMaxPf; ++q) {
+                const int t = tid + q * NT;
+                pf[q] = (inew < nf && t < W * 36) ? d.Bd[((size_t)inew * W) * 36 + t] : 0.0;
+            }
+            pfb = (inew < nf && tid < 6) ? d.bs[(size_t)inew * 6 + tid] : 0.0;
+        }
+        // ---- phase A: S_k^{-1} by Gauss–Jordan (wave 0, lane = r*6+c), z_k = S_k^{-1} y_k
+        if (tid < 64) {
+            const int lane = tid, r = lane / 6, c = lane % 6;
+            const bool act = lane < 36;
+            double M = act ? win[((size_t)sk * W + 0) * 36 + lane] : 0.0;
+            double I = (act && r == c) ? 1.0 : 0.0;
+            bool fail = false;
+#pragma unroll
+            for (int p = 0; p < 6; ++p) {
+                const double piv = __shfl(M, 7 * p, 64);
+                const double f = __shfl(M, (act ? r : 0) * 6 + p, 64);
+                double mp = __shfl(M, p * 6 + (act ? c : 0), 64);
+                double ip = __shfl(I, p * 6 + (act ? c : 0), 64);
+                if (piv == 0.0) fail = true;
+                mp = mp / piv;
+                ip = ip / piv;
+                if (r == p) { M = mp; I = ip; }
+                else { M = M - f * mp; I = I - f * ip; }
+            }
+            if (act) {
+                Kv[lane] = I;
+                d.Kinv[(size_t)k * 36 + lane] = I;
+            }
+            if (fail && lane == 0) s_fail = 1;
+            double yv = (lane < 6) ? bwin[sk * 6 + lane] : 0.0;
+            if (lane < 6) yk[lane] = yv;
+            double z = 0.0;
+#pragma unroll
+            for (int m = 0; m < 6; ++m) z += __shfl(I, (lane < 6 ? lane : 0) * 6 + m, 64) * __shfl(yv, m, 64);
+            if (lane < 6) d.zb[(size_t)k * 6 + lane] = z;
+        }
+        __syncthreads();
+        if (s_fail) break;
+        const int wmax = min(bw, nf - 1 - k);
+        // ---- phase B: L_{k+w,k} = A_{k+w,k} S_k^{-1}
+        for (int t = tid; t < wmax * 36; t += NT) {
+            const int w = 1 + t / 36, e = t % 36, r = e / 6, c = e % 6;
+            const int i = k + w;
+            double v = 0.0;
+            if (d.first_blk[i] <= k) {
+                const double *Aik = win + ((size_t)(i % W) * W + w) * 36;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) v += Aik[r * 6 + m] * Kv[m * 6 + c];
+            }
+            Lcol[w * 36 + e] = v;
+            d.Lband[((size_t)i * W + w) * 36 + e] = v;
+        }
+        __syncthreads();
+        // ---- phase C: trailing update A_ij -= L_ik A_jkᵀ, b_i -= L_ik y_k ; refill slot sk
+        const int npairs = wmax * (wmax + 1) / 2;
+        for (int t = tid; t < npairs * 36; t += NT) {
+            const int pr = t / 36, e = t % 36, r = e / 6, c = e % 6;
+            // pair index -> (wi >= wj >= 1)
+            const int wi = (int)((sqrt(8.0 * pr + 1.0) - 1.0) * 0.5) + 1;
+            const int wj = pr - (wi - 1) * wi / 2 + 1;
+            const int i = k + wi, j = k + wj;
+            if (d.first_blk[i] > k || d.first_blk[j] > k) continue;
+            const double *Li = Lcol + wi * 36;
+            const double *Ajk = win + ((size_t)(j % W) * W + wj) * 36;
+            double s = 0.0;
+#pragma unroll
+            for (int m = 0; m < 6; ++m) s += Li[r * 6 + m] * Ajk[c * 6 + m];
+            win[((size_t)(i % W) * W + (wi - wj)) * 36 + e] -= s;
+        }
+        for (int t = tid; t < wmax * 6; t += NT) {
+            const int wi = 1 + t / 6, r = t % 6, i = k + wi;
+            if (d.first_blk[i] > k) continue;
+            double s = 0.0;
+#pragma unroll
+            for (int m = 0; m < 6; ++m) s += Lcol[wi * 36 + r * 6 + m] * yk[m];
+            bwin[(i % W) * 6 + r] -= s;
+        }
+#pragma unroll
+        for (int q = 0; q < kMaxPf; ++q) {
+            const int t = tid + q * NT;
+            if (t < W * 36) win[(size_t)sk * W * 36 + t] = pf[q];
+        }
+        if (tid < 6) bwin[sk * 6 + tid] = pfb;
+        __syncthreads();
+    }
+    if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
+    if (s_fail) return;
+    // ---- backward: x_k = z_k - Σ_w L_{k+w,k}ᵀ x_{k+w}   (wave 0, no barriers; L prefetched)
+    if (tid < 64) {
+        const int lane = tid;
+        constexpr int kMaxB = (kBandMax * 6 + 63) / 64;
+        double Lc[kMaxB][6], Ln[kMaxB][6];
+        auto load_L = [&](int k, double (&dst)[kMaxB][6]) {
+            const int wmax = (k >= 0) ? min(bw, nf - 1 - k) : 0;
+#pragma unroll
+            for (int q = 0; q < kMaxB; ++q) {
+                const int t = q * 64 + lane;
+                const int w = 1 + t / 6, r = t % 6;
+                const bool ok = t < wmax * 6;
+                const double *L = d.Lband + ((size_t)(k + w) * W + w) * 36;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) dst[q][m] = ok ? L[m * 6 + r] : 0.0;
+            }
+        };
+        load_L(nf - 1, Lc);
+        for (int k = nf - 1; k >= 0; --k) {
+            const int wmax = min(bw, nf - 1 - k);
+            load_L(k - 1, Ln);
+            const double zk = (lane < 6) ? d.zb[(size_t)k * 6 + lane] : 0.0;
+#pragma unroll
+            for (int q = 0; q < kMaxB; ++q) {
+                const int t = q * 64 + lane;
+                if (t < wmax * 6) {
+                    const int w = 1 + t / 6, r = t % 6, i = k + w;
+                    const double *x = xr + (i % W) * 6;
+                    double s = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) s += Lc[q][m] * x[m];
+                    part[w * 6 + r] = s;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 6) {
+                double v = zk;
+                for (int w = 1; w <= wmax; ++w) v -= part[w * 6 + lane];
+                xr[(k % W) * 6 + lane] = v;
+                d.xp[(size_t)k * 6 + lane] = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int q = 0; q < kMaxB; ++q)
+#pragma unroll
+                for (int m = 0; m < 6; ++m) Lc[q][m] = Ln[q][m];
+        }
+    }
 }
 
 // ---------------------------------------------------------------- update + trial evaluation

@@ -16,10 +16,10 @@ def rel_err(a, b):
 
 def row_rel_err(a, b):
     """max over rows of |a_i-b_i| / max(|b_i|, 1): per-landmark relative error."""
+    if len(b) == 0:
+        return 0.0
     a = np.asarray(a, np.float64).reshape(len(a), -1)
     b = np.asarray(b, np.float64).reshape(len(b), -1)
-    if b.size == 0:
-        return 0.0
     num = np.abs(a - b).max(axis=1)
     den = np.maximum(np.abs(b).max(axis=1), 1.0)
     return float((num / den).max())

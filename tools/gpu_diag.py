@@ -32,6 +32,9 @@ for cfg in cfgs:
     print(f"== {cfg}: E={g.n_ept}+{g.n_eln} gen {t1-t0:.2f}s oracle {ref['solve_ms']:.1f}ms upload {1e3*(t3-t2):.1f}ms "
           f"gpu {out['solve_ms']:.2f}ms / {out2['solve_ms']:.2f}ms iters gpu {out['iters']} ref {ref['iters']}", flush=True)
     print("   metrics", m, flush=True)
+    print("   depth flags equal:", np.array_equal(out["ept_depth_ok"], ref["ept_depth_ok"]),
+          "gpu bad", int((out["ept_depth_ok"] == 0).sum()), "ref bad", int((ref["ept_depth_ok"] == 0).sum()),
+          "chi2 rel", float(np.abs(out["ept_chi2"] - ref["ept_chi2"]).max() / max(ref["ept_chi2"].max(), 1e-30)))
     print("   deterministic rerun:", all(np.array_equal(out[k], out2[k]) for k in ("kf_Tcw", "pt_xyz", "ln_orth")))
     for a, b in zip(out["trace"], ref["trace"]):
         print(f"   st{a['stage']} it{a['iter']:2d} gpu chi {a['chi2_start']:.10g}->{a['chi2_end']:.10g} lam {a['lambda_end']:.4g} tr {a['trials']} | "
