@@ -18,6 +18,7 @@
 #include <map>
 #include <numeric>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/plba.h"
@@ -116,7 +117,31 @@ namespace {
 inline int blocks_for(int n, int b = kBlock) { return (n + b - 1) / b; }
 inline size_t band_lds_bytes(int bw) {
     const size_t W = bw + 1;
-    return sizeof(double) * (W * W * 36 + W * 6 + W * 36 + 36 + W * 6 + W * 6 + 6);
+    return sizeof(double) * (W * W * 36 + W * 6 + W * 36 + 72 + W * 6 + W * 6 + 12);
+}
+template <int... B>
+const void *band_kernel_impl(int bw, std::integer_sequence<int, B...>) {
+    const void *k = nullptr;
+    ((bw == B ? (k = (const void *)k_rcs_factor_band<B>, 0) : 0), ...);
+    return k;
+}
+inline const void *band_kernel(int bw) {
+    return band_kernel_impl(bw, std::make_integer_sequence<int, kBandMax + 1>{});
+}
+inline void launch_band(Dev &d, size_t lds, hipStream_t s) {
+    const void *k = band_kernel(d.bw);
+    void *args[] = {&d};
+    (void)hipLaunchKernel(k, dim3(1), dim3(kBandNT), args, lds, s);
+}
+inline int band_ring(int bw, int nf) {
+    const size_t budget = 150 * 1024, base = band_lds_bytes(bw);
+    const size_t per = sizeof(double) * ((size_t)bw * 36 + 36 + 6);
+    int R = base + per < budget ? (int)((budget - base - per) / per) : 1;
+    return std::max(1, std::min(R, 16));
+}
+inline size_t band_lds_bytes(int bw, int nf) {
+    const int R = band_ring(bw, nf);
+    return band_lds_bytes(bw) + sizeof(double) * ((size_t)R * bw * 36 + (size_t)(R + 1) * (36 + 6));
 }
 
 // time a launch when kernel timing is enabled
@@ -341,6 +366,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.nf = nf; d.n = n; d.nblk = nblk; d.ntiles = ntiles;
     d.bw = bw;
     d.band_mode = band_mode ? 1 : 0;
+    d.ring = band_ring(bw, nf);
     d.corrected = ctx->opts.corrected_line_jacobian;
     d.robust = 1;
     d.cam = Cam{g->fx, g->fy, g->cx, g->cy};
@@ -419,14 +445,14 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_ps, d.n_kf_blocks);
     ALLOC(d.ctrl, 1);
     ALLOC(ctx->d_depth, Ep);
+#ifdef PLBA_STAMPS
+    ALLOC(d.stamps, 16 * 8);
+    PLBA_CHECK(hipMemset(d.stamps, 0, 16 * 8 * sizeof(unsigned long long)));
+#endif
 #undef ALLOC
 #undef UPLOAD
-    if (band_mode) {
-        PLBA_CHECK(hipFuncSetAttribute((const void *)k_rcs_factor_band<256>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_lds_bytes(bw)));
-        PLBA_CHECK(hipFuncSetAttribute((const void *)k_rcs_factor_band<1024>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)band_lds_bytes(bw)));
-    }
+    if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  (int)band_lds_bytes(bw, nf)));
     PLBA_CHECK(hipMemset(d.e_level, 0, E));
     PLBA_CHECK(hipMemset(d.xp, 0, sizeof(double) * std::max(n, 1)));
     PLBA_CHECK(hipMemset(d.xl, 0, sizeof(double) * std::max(n_lm, 1) * 4));
@@ -441,9 +467,12 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 int do_initialize(plba_ctx *ctx, int level) {
     Dev &d = ctx->d;
     d.robust = ctx->robust;
-    if (d.E > 0) hipLaunchKernelGGL(k_activate_edges, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d, level);
-    int nv = std::max(d.n_lm, d.n_kf);
-    if (nv > 0) hipLaunchKernelGGL(k_activate_vertices, dim3(blocks_for(nv)), dim3(kBlock), 0, ctx->stream, d);
+    if (d.n_lm) PLBA_CHECK(hipMemsetAsync(d.lm_active, 0, d.n_lm, ctx->stream));
+    if (d.n_kf) PLBA_CHECK(hipMemsetAsync(d.kf_active, 0, d.n_kf, ctx->stream));
+    if (d.E > 0) {
+        hipLaunchKernelGGL(k_activate_edges, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d, level);
+        hipLaunchKernelGGL(k_activate_vertices, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d);
+    }
     PLBA_CHECK(hipGetLastError());
     ctx->level = level;
     ctx->initialized = true;
@@ -472,10 +501,8 @@ int lm_iteration(plba_ctx *ctx, int it) {
             if (!d.band_mode)
                 LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
             LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_assemble, dim3(blocks_for(d.nblk * 64)), dim3(kBlock), 0, s, d));
-            if (d.band_mode && d.bw <= 8)
-                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor_band<256>, dim3(1), dim3(256), band_lds_bytes(d.bw), s, d));
-            else if (d.band_mode)
-                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor_band<1024>, dim3(1), dim3(1024), band_lds_bytes(d.bw), s, d));
+            if (d.band_mode)
+                LAUNCH(K_FACTOR, launch_band(d, band_lds_bytes(d.bw, d.nf), s));
             else
                 LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
         } else {
@@ -778,6 +805,18 @@ int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *la
         if (launches) launches[k] = ctx->k_n[k];
     }
     return PLBA_OK;
+}
+
+// Diagnostic build only: per-wave, per-phase cycle sums of the banded factorisation.
+int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [16][8] */) {
+#ifdef PLBA_STAMPS
+    if (!ctx || !ctx->d.stamps) return PLBA_E_STATE;
+    PLBA_CHECK(hipMemcpy(out, ctx->d.stamps, 16 * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return PLBA_OK;
+#else
+    (void)ctx; (void)out;
+    return PLBA_E_STATE;
+#endif
 }
 
 // Extension: enable per-kernel HIP-event timing for subsequent plba_lba_plucker calls.

@@ -27,6 +27,10 @@ namespace plba {
 constexpr int kBlock = 256;
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
 constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window factorisation holds
+#ifndef PLBA_BAND_NT
+#define PLBA_BAND_NT 1024
+#endif
+constexpr int kBandNT = PLBA_BAND_NT; // threads of the banded factorisation workgroup
 
 struct Ctrl {
     double lambda, ni, currentChi, tempChi, rho, scale, maxdiag;
@@ -68,6 +72,8 @@ struct Dev {
     int32_t *tile_last;                 // [ntiles] last row tile whose envelope reaches column tile K
     // block-band storage (used when the envelope bandwidth bw <= kBandMax)
     int32_t bw, band_mode;              // bandwidth in pose blocks; 1 = banded factorisation
+    int32_t ring;                       // steps of L / S^-1 / z staged in LDS between global flushes
+    unsigned long long *stamps;         // diagnostic build only (PLBA_STAMPS): per-phase cycle sums
     int32_t *first_blk;                 // [nf] first block column of each block row (lower)
     double *Bd;                         // [nf][bw+1][36]  block (i, i-w), row-major 6x6
     double *Lband;                      // [nf][bw+1][36]  L_{i,i-w} (w >= 1)
@@ -118,24 +124,37 @@ __device__ __forceinline__ double block_max(double v, double *sh) {
 }
 __device__ __forceinline__ bool is_point_lm(const Dev &d, int lm) { return lm < d.n_pt; }
 
+#ifdef PLBA_STAMPS
+#define STAMP(slot)                                                                         \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        unsigned long long _t;                                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        if ((threadIdx.x & 63) == 0) { st_acc[slot] += _t - st_last; }                      \
+        st_last = _t;                                                                       \
+    } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
+
+// Workgroup barrier that orders LDS only: global stores/prefetch loads stay in flight across it
+// (__syncthreads() would drain vmcnt and put an L2 round trip on every step of a serial chain).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ---------------------------------------------------------------- activation
 __global__ void k_activate_edges(Dev d, int level) {
     int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < d.E) d.e_active[e] = (d.e_level[e] == level) ? 1 : 0;
 }
+// vertices are active iff they have an active edge (writes of the constant 1 only: race-free)
 __global__ void k_activate_vertices(Dev d) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < d.n_lm) {
-        uint8_t a = 0;
-        for (int e = d.lm_off[i]; e < d.lm_off[i + 1]; ++e) a |= d.e_active[e];
-        d.lm_active[i] = a;
-    }
-    if (i < d.n_kf) {
-        int h = d.kf_hidx[i];
-        uint8_t a = 0;
-        if (h >= 0)
-            for (int p = d.pe_off[h]; p < d.pe_off[h + 1]; ++p) a |= d.e_active[d.pe_list[p]];
-        d.kf_active[i] = a;
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < d.E && d.e_active[e]) {
+        d.lm_active[d.e_lm[e]] = 1;
+        d.kf_active[d.e_kf[e]] = 1;
     }
 }
 
@@ -610,131 +629,269 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
 // then a one-wave backward pass. One workgroup; 3 barriers per pose block.
 // Failure semantics of SimplicialLDLT: a zero pivot (Gauss–Jordan pivots of S_k are the LDLᵀ
 // pivots) fails the solve and x_p keeps its previous value.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_rcs_factor_band(Dev d) {
+// fast IEEE-accurate reciprocal: v_rcp_f64 + two Newton steps
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return r;
+}
+// Gauss–Jordan on [S | y] (6x7, one entry per lane): lanes r*6+c (0..35) hold S and return
+// S^{-1}; lanes 36+r hold y and return z = S^{-1} y. No pivoting: the pivots are the LDLᵀ
+// pivots, so a zero pivot reports failure exactly as SimplicialLDLT's NumericalIssue does.
+__device__ __forceinline__ double gj_inverse6(double M, int lane, bool &fail) {
+    const bool mat = lane < 36, rhs = lane >= 36 && lane < 42;
+    const int r = mat ? lane / 6 : (rhs ? lane - 36 : 0);
+    const int c = mat ? lane % 6 : 0;
+    double I = (mat && r == c) ? 1.0 : (rhs ? M : 0.0);  // rhs lanes carry y in I
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+        const double piv = __shfl(M, 7 * p, 64);
+        const double f = __shfl(M, r * 6 + p, 64);
+        double ip = __shfl(I, rhs ? 36 + p : p * 6 + c, 64);
+        double mp = __shfl(M, p * 6 + c, 64);
+        if (piv == 0.0) fail = true;
+        const double rp = rcp_nr(piv);
+        mp = mp * rp;
+        ip = ip * rp;
+        if (r == p) { M = mp; I = ip; }
+        else { M = fma(-f, mp, M); I = fma(-f, ip, I); }
+    }
+    return I;
+}
+
+// Block-banded LDLᵀ with lookahead, templated on the envelope bandwidth BW (pose blocks).
+// Wave 0 carries the critical chain
+//   S_k^{-1} -> L_{k+1,k} -> S_{k+1} = A_{k+1,k+1} - L_{k+1,k} A_{k+1,k}ᵀ -> S_{k+1}^{-1}
+// while waves 1..15 compute the other L blocks and the trailing updates of step k
+// (2 LDS-only barriers per step). Each worker's entries and LDS offsets are compile-time /
+// hoisted; window slots advance incrementally (no runtime modulo in the loop).
+template <int BW>
+__global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
+    constexpr int NT = kBandNT, W = BW + 1, NW = NT - 64;
+    constexpr int NPAIR = BW * (BW + 1) / 2;             // trailing (wi >= wj >= 1) block pairs
+    constexpr int PPT0 = (NPAIR * 36 - 36 + NW - 1) / NW; // pair entries per worker (pair 0 = wave 0)
+    constexpr int PPT = PPT0 > 0 ? PPT0 : 1;
+    constexpr int LPT = ((BW > 1 ? BW - 1 : 0) * 36 + NW - 1) / NW;  // L entries per worker (w >= 2)
+    constexpr int RFT = (W * 36 + NW - 1) / NW;           // refill entries per worker
+    constexpr int NPT = (NPAIR * 36 > 36) ? NPAIR * 36 : 36; // valid pair-entry bound
     extern __shared__ double lds[];
-    const int bw = d.bw, W = bw + 1, nf = d.nf;
-    double *win = lds;                          // [W slots][W][36]
-    double *bwin = win + (size_t)W * W * 36;    // [W][6]
-    double *Lcol = bwin + (size_t)W * 6;        // [W][36]  (index w = 1..bw)
-    double *Kv = Lcol + (size_t)W * 36;         // [36]
-    double *xr = Kv + 36;                       // [W][6]  ring of solved x blocks
-    double *part = xr + (size_t)W * 6;          // [W][6]
-    double *yk = part + (size_t)W * 6;          // [6]  y_k snapshot (slot sk is refilled in phase C)
+    const int nf = d.nf;
+    double *win = lds;                            // [W slots][W][36]
+    double *bwin = win + (size_t)W * W * 36;      // [W][6]
+    double *Lcol = bwin + (size_t)W * 6;          // [W][36]  (index w = 1..BW)
+    double *Kv = Lcol + (size_t)W * 36;           // [2][36]  S_k^{-1} double buffer
+    double *xr = Kv + 72;                         // [W][6]  ring of solved x blocks
+    double *part = xr + (size_t)W * 6;            // [W][6]
+    double *ys = part + (size_t)W * 6;            // [2][6]  y_k snapshots
+    const int R = d.ring;
+    const int RK = R + 1;                         // S^-1 / z of step k+1 are written during step k
+    double *ringL = ys + 12;                      // [R][BW][36]
+    double *ringK = ringL + (size_t)R * BW * 36;  // [RK][36]
+    double *ringZ = ringK + (size_t)RK * 36;      // [RK][6]
     __shared__ int s_fail;
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const bool crit = tid < 64;                   // wave 0
+    const int wt = tid - 64;                      // worker thread index
     if (tid == 0) s_fail = 0;
-    // initial window: rows 0..min(bw, nf-1)
     for (int t = tid; t < W * W * 36; t += NT) {
         const int row = t / (W * 36), rem = t % (W * 36);
         win[t] = (row < nf) ? d.Bd[((size_t)row * W) * 36 + rem] : 0.0;
     }
     for (int t = tid; t < W * 6; t += NT) bwin[t] = (t / 6 < nf) ? d.bs[t] : 0.0;
-    // refill prefetch registers: thread t owns entries t, t+NT, ... of one W*36 block row (+6 of b)
-    constexpr int kMaxPf = (kBandMax + 1) * 36 / NT + 1;
-    double pf[kMaxPf];
-    double pfb = 0.0;
-    __syncthreads();
-    for (int k = 0; k < nf; ++k) {
-        const int sk = k % W;
-        {   // issue the loads of block row k+W now; they land in LDS in phase C
-            const int inew = k + W;
+    // ---- per-worker static assignment
+    int p_wi[PPT], p_wj[PPT], p_li[PPT], p_aj[PPT], p_dst[PPT];
 #pragma unroll
-            for (int q = 0; q < kMaxPf; ++q) {
-                const int t = tid + q * NT;
-                pf[q] = (inew < nf && t < W * 36) ? d.Bd[((size_t)inew * W) * 36 + t] : 0.0;
-            }
-            pfb = (inew < nf && tid < 6) ? d.bs[(size_t)inew * 6 + tid] : 0.0;
-        }
-        // ---- phase A: S_k^{-1} by Gauss–Jordan (wave 0, lane = r*6+c), z_k = S_k^{-1} y_k
-        if (tid < 64) {
-            const int lane = tid, r = lane / 6, c = lane % 6;
-            const bool act = lane < 36;
-            double M = act ? win[((size_t)sk * W + 0) * 36 + lane] : 0.0;
-            double I = (act && r == c) ? 1.0 : 0.0;
-            bool fail = false;
-#pragma unroll
-            for (int p = 0; p < 6; ++p) {
-                const double piv = __shfl(M, 7 * p, 64);
-                const double f = __shfl(M, (act ? r : 0) * 6 + p, 64);
-                double mp = __shfl(M, p * 6 + (act ? c : 0), 64);
-                double ip = __shfl(I, p * 6 + (act ? c : 0), 64);
-                if (piv == 0.0) fail = true;
-                mp = mp / piv;
-                ip = ip / piv;
-                if (r == p) { M = mp; I = ip; }
-                else { M = M - f * mp; I = I - f * ip; }
-            }
-            if (act) {
-                Kv[lane] = I;
-                d.Kinv[(size_t)k * 36 + lane] = I;
-            }
-            if (fail && lane == 0) s_fail = 1;
-            double yv = (lane < 6) ? bwin[sk * 6 + lane] : 0.0;
-            if (lane < 6) yk[lane] = yv;
-            double z = 0.0;
-#pragma unroll
-            for (int m = 0; m < 6; ++m) z += __shfl(I, (lane < 6 ? lane : 0) * 6 + m, 64) * __shfl(yv, m, 64);
-            if (lane < 6) d.zb[(size_t)k * 6 + lane] = z;
-        }
-        __syncthreads();
-        if (s_fail) break;
-        const int wmax = min(bw, nf - 1 - k);
-        // ---- phase B: L_{k+w,k} = A_{k+w,k} S_k^{-1}
-        for (int t = tid; t < wmax * 36; t += NT) {
-            const int w = 1 + t / 36, e = t % 36, r = e / 6, c = e % 6;
-            const int i = k + w;
-            double v = 0.0;
-            if (d.first_blk[i] <= k) {
-                const double *Aik = win + ((size_t)(i % W) * W + w) * 36;
-#pragma unroll
-                for (int m = 0; m < 6; ++m) v += Aik[r * 6 + m] * Kv[m * 6 + c];
-            }
-            Lcol[w * 36 + e] = v;
-            d.Lband[((size_t)i * W + w) * 36 + e] = v;
-        }
-        __syncthreads();
-        // ---- phase C: trailing update A_ij -= L_ik A_jkᵀ, b_i -= L_ik y_k ; refill slot sk
-        const int npairs = wmax * (wmax + 1) / 2;
-        for (int t = tid; t < npairs * 36; t += NT) {
-            const int pr = t / 36, e = t % 36, r = e / 6, c = e % 6;
-            // pair index -> (wi >= wj >= 1)
-            const int wi = (int)((sqrt(8.0 * pr + 1.0) - 1.0) * 0.5) + 1;
-            const int wj = pr - (wi - 1) * wi / 2 + 1;
-            const int i = k + wi, j = k + wj;
-            if (d.first_blk[i] > k || d.first_blk[j] > k) continue;
-            const double *Li = Lcol + wi * 36;
-            const double *Ajk = win + ((size_t)(j % W) * W + wj) * 36;
-            double s = 0.0;
-#pragma unroll
-            for (int m = 0; m < 6; ++m) s += Li[r * 6 + m] * Ajk[c * 6 + m];
-            win[((size_t)(i % W) * W + (wi - wj)) * 36 + e] -= s;
-        }
-        for (int t = tid; t < wmax * 6; t += NT) {
-            const int wi = 1 + t / 6, r = t % 6, i = k + wi;
-            if (d.first_blk[i] > k) continue;
-            double s = 0.0;
-#pragma unroll
-            for (int m = 0; m < 6; ++m) s += Lcol[wi * 36 + r * 6 + m] * yk[m];
-            bwin[(i % W) * 6 + r] -= s;
-        }
-#pragma unroll
-        for (int q = 0; q < kMaxPf; ++q) {
-            const int t = tid + q * NT;
-            if (t < W * 36) win[(size_t)sk * W * 36 + t] = pf[q];
-        }
-        if (tid < 6) bwin[sk * 6 + tid] = pfb;
-        __syncthreads();
+    for (int q = 0; q < PPT; ++q) {
+        const int t = wt + 36 + q * NW;
+        int pr = t / 36, e = t % 36, wi = 1;
+        while ((wi * (wi + 1)) / 2 <= pr) ++wi;
+        const int wj = pr - (wi - 1) * wi / 2 + 1;
+        const bool ok = !crit && t < NPT && NPAIR > 1;
+        p_wi[q] = ok ? wi : 1 << 20;               // never <= wmax when invalid
+        p_wj[q] = wj;
+        p_li[q] = wi * 36 + (e / 6) * 6;
+        p_aj[q] = wj * 36 + (e % 6) * 6;
+        p_dst[q] = (wi - wj) * 36 + e;
     }
+    int l_w[LPT > 0 ? LPT : 1], l_e[LPT > 0 ? LPT : 1];
+#pragma unroll
+    for (int q = 0; q < LPT; ++q) {
+        const int t = wt + 36 + q * NW;
+        l_w[q] = (!crit && t < BW * 36) ? 1 + t / 36 : 1 << 20;
+        l_e[q] = t % 36;
+    }
+    double pf[RFT], pfn[RFT];
+    double pfb = 0.0, pfbn = 0.0;
+    auto prefetch = [&](int row, double (&dst)[RFT], double &dstb) {
+        const int rr = min(row, nf - 1);
+#pragma unroll
+        for (int q = 0; q < RFT; ++q) dst[q] = d.Bd[((size_t)rr * W) * 36 + min(max(wt, 0) + q * NW, W * 36 - 1)];
+        dstb = d.bs[(size_t)rr * 6 + min(max(wt, 0), 5)];
+    };
+    if (!crit) prefetch(W, pfn, pfbn);
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(tid) < 64) __builtin_amdgcn_s_setprio(3);
+    // S_0^{-1}, y_0, z_0
+    if (crit) {
+        bool fail = false;
+        double M = 0.0;
+        if (lane < 36) M = win[lane];
+        else if (lane < 42) { M = bwin[lane - 36]; ys[lane - 36] = M; }
+        const double I = gj_inverse6(M, lane, fail);
+        if (lane < 36) { Kv[lane] = I; ringK[lane] = I; }
+        else if (lane < 42) ringZ[lane - 36] = I;
+        if (fail && lane == 0) s_fail = 1;
+    }
+    lds_barrier();
+#ifdef PLBA_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
+    int sk = 0, kR = 0, kRK = 1;                  // k % W, k % R, (k+1) % RK
+    for (int k = 0; k < nf; ++k) {
+        if (s_fail) break;
+        const int kb = k & 1;
+        const int wmax = min(BW, nf - 1 - k);
+        const double *Kk = Kv + kb * 36;
+        const double *yk = ys + kb * 6;
+        auto slot = [&](int w) { const int x = sk + w; return x >= W ? x - W : x; };
+        if (!crit) {
+#pragma unroll
+            for (int q = 0; q < RFT; ++q) pf[q] = pfn[q];
+            pfb = pfbn;
+            prefetch(k + 1 + W, pfn, pfbn);
+        }
+        STAMP(0);
+        // ---- phase 1: L_{k+w,k} = A_{k+w,k} S_k^{-1}   (w = 1 on wave 0, w >= 2 on the workers)
+        if (crit) {
+            if (lane < 36 && wmax >= 1) {
+                const int c = lane % 6;
+                const double *Aik = win + ((size_t)slot(1) * W + 1) * 36 + (lane / 6) * 6;
+                double v = 0.0;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) v = fma(Aik[m], Kk[m * 6 + c], v);
+                Lcol[36 + lane] = v;
+                ringL[((size_t)kR * BW + 0) * 36 + lane] = v;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < LPT; ++q) {
+                const int w = l_w[q], e = l_e[q];
+                if (w <= wmax) {
+                    const double *Aik = win + ((size_t)slot(w) * W + w) * 36 + (e / 6) * 6;
+                    const int c = e % 6;
+                    double v = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) v = fma(Aik[m], Kk[m * 6 + c], v);
+                    Lcol[w * 36 + e] = v;
+                    ringL[((size_t)kR * BW + (w - 1)) * 36 + e] = v;
+                }
+            }
+        }
+        STAMP(1);
+        lds_barrier();
+        STAMP(2);
+        // ---- phase 2
+        if (crit) {
+            if (k + 1 < nf) {
+                const int s1 = slot(1), k1b = kb ^ 1;
+                // lanes 0..35: S_{k+1} = A_{k+1,k+1} - L_{k+1,k} A_{k+1,k}ᵀ
+                // lanes 36..41: y_{k+1} = b_{k+1} - L_{k+1,k} y_k
+                double M = 0.0;
+                if (lane < 42) {
+                    const bool mat = lane < 36;
+                    const int r = mat ? lane / 6 : lane - 36, c = mat ? lane % 6 : 0;
+                    double sacc = 0.0;
+                    if constexpr (BW >= 1) {
+                        const double *L1 = Lcol + 36 + r * 6;
+                        const double *A1 = mat ? win + ((size_t)s1 * W + 1) * 36 + c * 6 : yk;
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) sacc = fma(L1[m], A1[m], sacc);
+                    }
+                    double *dst = mat ? win + ((size_t)s1 * W + 0) * 36 + lane : bwin + s1 * 6 + r;
+                    M = *dst - sacc;
+                    *dst = M;
+                    if (!mat) ys[k1b * 6 + r] = M;
+                }
+                bool fail = false;
+                const double I = gj_inverse6(M, lane, fail);
+                if (lane < 36) { Kv[k1b * 36 + lane] = I; ringK[kRK * 36 + lane] = I; }
+                else if (lane < 42) ringZ[kRK * 6 + lane - 36] = I;
+                if (fail && lane == 0) s_fail = 1;
+            }
+        } else {
+            // trailing update A_ij -= L_ik A_jkᵀ for all pairs (wi >= wj >= 1) except (1,1)
+#pragma unroll
+            for (int q = 0; q < PPT; ++q) {
+                const int wi = p_wi[q];
+                if (wi <= wmax) {
+                    const double *Li = Lcol + p_li[q];
+                    const double *Ajk = win + (size_t)slot(p_wj[q]) * W * 36 + p_aj[q];
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) sacc = fma(Li[m], Ajk[m], sacc);
+                    win[(size_t)slot(wi) * W * 36 + p_dst[q]] -= sacc;
+                }
+            }
+            STAMP(5);
+            // b_i -= L_ik y_k for w >= 2 (last worker wave)
+            {
+                const int t = NW - 1 - wt;  // 0.. on the last wave
+                if (t < (wmax - 1) * 6) {
+                    const int wi = 2 + t / 6, r = t % 6;
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) sacc = fma(Lcol[wi * 36 + r * 6 + m], yk[m], sacc);
+                    bwin[slot(wi) * 6 + r] -= sacc;
+                }
+            }
+            STAMP(6);
+            if (kR == R - 1 || k == nf - 1) {  // flush the staged steps k0..k to global
+                const int k0 = k - kR;
+                const int cnt = kR + 1;
+                for (int t = wt; t < cnt * BW * 36; t += NW) {
+                    const int st = t / (BW * 36), rem = t % (BW * 36), w = 1 + rem / 36, e = rem % 36;
+                    const int i = k0 + st + w;
+                    if (i < nf) d.Lband[((size_t)i * W + w) * 36 + e] = ringL[(size_t)st * BW * 36 + rem];
+                }
+                for (int t = wt; t < cnt * 36; t += NW)
+                    d.Kinv[(size_t)k0 * 36 + t] = ringK[((k0 + t / 36) % RK) * 36 + t % 36];
+                for (int t = wt; t < cnt * 6; t += NW) d.zb[(size_t)k0 * 6 + t] = ringZ[((k0 + t / 6) % RK) * 6 + t % 6];
+            }
+            STAMP(7);
+            // block row k+W enters slot sk (row k is fully consumed)
+            const bool live = k + W < nf;
+#pragma unroll
+            for (int q = 0; q < RFT; ++q) {
+                const int t = wt + q * NW;
+                if (t < W * 36) win[(size_t)sk * W * 36 + t] = live ? pf[q] : 0.0;
+            }
+            if (wt < 6) bwin[sk * 6 + wt] = live ? pfb : 0.0;
+        }
+        STAMP(3);
+        lds_barrier();
+        STAMP(4);
+        sk = (sk + 1 == W) ? 0 : sk + 1;
+        kR = (kR + 1 == R) ? 0 : kR + 1;
+        kRK = (kRK + 1 == RK) ? 0 : kRK + 1;
+    }
+#ifdef PLBA_STAMPS
+    if ((tid & 63) == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&d.stamps[(tid >> 6) * 8 + q], st_acc[q]);
+#endif
+    __syncthreads();  // drains every wave's flush stores: the backward pass reads them
     if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
     if (s_fail) return;
     // ---- backward: x_k = z_k - Σ_w L_{k+w,k}ᵀ x_{k+w}   (wave 0, no barriers; L prefetched)
     if (tid < 64) {
         const int lane = tid;
-        constexpr int kMaxB = (kBandMax * 6 + 63) / 64;
+        constexpr int kMaxB = (BW * 6 + 63) / 64 > 0 ? (BW * 6 + 63) / 64 : 1;
         double Lc[kMaxB][6], Ln[kMaxB][6];
         auto load_L = [&](int k, double (&dst)[kMaxB][6]) {
-            const int wmax = (k >= 0) ? min(bw, nf - 1 - k) : 0;
+            const int wmax = (k >= 0) ? min(BW, nf - 1 - k) : 0;
 #pragma unroll
             for (int q = 0; q < kMaxB; ++q) {
                 const int t = q * 64 + lane;
@@ -746,10 +903,12 @@ __global__ __launch_bounds__(NT) void k_rcs_factor_band(Dev d) {
             }
         };
         load_L(nf - 1, Lc);
+        double zc = (lane < 6) ? d.zb[(size_t)(nf - 1) * 6 + lane] : 0.0, zn;
         for (int k = nf - 1; k >= 0; --k) {
-            const int wmax = min(bw, nf - 1 - k);
+            const int wmax = min(BW, nf - 1 - k);
             load_L(k - 1, Ln);
-            const double zk = (lane < 6) ? d.zb[(size_t)k * 6 + lane] : 0.0;
+            zn = (lane < 6 && k > 0) ? d.zb[(size_t)(k - 1) * 6 + lane] : 0.0;
+            const double zk = zc;
 #pragma unroll
             for (int q = 0; q < kMaxB; ++q) {
                 const int t = q * 64 + lane;
@@ -776,6 +935,7 @@ __global__ __launch_bounds__(NT) void k_rcs_factor_band(Dev d) {
             for (int q = 0; q < kMaxB; ++q)
 #pragma unroll
                 for (int m = 0; m < 6; ++m) Lc[q][m] = Ln[q][m];
+            zc = zn;
         }
     }
 }

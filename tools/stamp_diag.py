@@ -1,0 +1,29 @@
+"""Per-phase cycle breakdown of k_rcs_factor_band from the PLBA_STAMPS diagnostic build."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pl-slam-plucker_amd"))
+import numpy as np  # noqa: E402
+
+from plba import lib, synth  # noqa: E402
+
+lib.load(os.path.join(ROOT, "pl-slam-plucker_amd", "libplba_stamps.so"))
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
+s = lib.Solver()
+g = synth.generate(cfg)
+s.upload(g)
+out = s.lba_plucker(want_outputs=False)
+buf = (C.c_ulonglong * 128)()
+rc = s.L.plba_debug_stamps(s.ctx, buf)
+a = np.array(buf[:], dtype=np.float64).reshape(16, 8)
+names = ["top(prefetch)", "phase1", "bar1", "ph2-end(refill|crit)", "bar2", "ph2-pairs", "ph2-b", "ph2-flush"]
+ntr = int(sum(t["trials"] for t in out["trace"]))
+nf = int((g.kf_fixed == 0).sum())
+print(cfg, "rc", rc, "trials", ntr, "steps", ntr * nf)
+for w in range(16):
+    if a[w].sum() == 0:
+        continue
+    per = a[w] / (ntr * nf)
+    print(f"wave {w:2d} cycles/step: " + " ".join(f"{n}={v:.0f}" for n, v in zip(names, per)), f"total={per.sum():.0f}")
