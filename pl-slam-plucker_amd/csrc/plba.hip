@@ -819,6 +819,15 @@ int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [16][8] */) {
 #endif
 }
 
+int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
+    if (!ctx || !out) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    const int64_t v[7] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+                          ctx->d.band_mode};
+    for (int i = 0; i < cap && i < 7; ++i) out[i] = v[i];
+    return PLBA_OK;
+}
+
 // Extension: enable per-kernel HIP-event timing for subsequent plba_lba_plucker calls.
 int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on) {
     if (!ctx) return PLBA_E_INVALID;

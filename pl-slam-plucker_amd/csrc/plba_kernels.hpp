@@ -852,11 +852,12 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
             if (kR == R - 1 || k == nf - 1) {  // flush the staged steps k0..k to global
                 const int k0 = k - kR;
                 const int cnt = kR + 1;
-                for (int t = wt; t < cnt * BW * 36; t += NW) {
-                    const int st = t / (BW * 36), rem = t % (BW * 36), w = 1 + rem / 36, e = rem % 36;
-                    const int i = k0 + st + w;
-                    if (i < nf) d.Lband[((size_t)i * W + w) * 36 + e] = ringL[(size_t)st * BW * 36 + rem];
-                }
+                if constexpr (BW >= 1)
+                    for (int t = wt; t < cnt * BW * 36; t += NW) {
+                        const int st = t / (BW * 36), rem = t % (BW * 36), w = 1 + rem / 36, e = rem % 36;
+                        const int i = k0 + st + w;
+                        if (i < nf) d.Lband[((size_t)i * W + w) * 36 + e] = ringL[(size_t)st * BW * 36 + rem];
+                    }
                 for (int t = wt; t < cnt * 36; t += NW)
                     d.Kinv[(size_t)k0 * 36 + t] = ringK[((k0 + t / 36) % RK) * 36 + t % 36];
                 for (int t = wt; t < cnt * 6; t += NW) d.zb[(size_t)k0 * 6 + t] = ringZ[((k0 + t / 6) % RK) * 6 + t % 6];

@@ -25,7 +25,7 @@ EXPORTED = [
     "plba_default_opts", "plba_create", "plba_destroy", "plba_last_error", "plba_upload", "plba_reset_estimates",
     "plba_set_edge_levels", "plba_set_robust", "plba_initialize_optimization", "plba_optimize",
     "plba_refresh_edge_errors", "plba_get_edge_chi2", "plba_download", "plba_lba_plucker", "plba_get_trace",
-    "plba_synchronize", "plba_enable_kernel_timing", "plba_kernel_times",
+    "plba_synchronize", "plba_enable_kernel_timing", "plba_kernel_times", "plba_structure_stats",
 ]
 
 
@@ -67,6 +67,7 @@ def load(path: Optional[str] = None):
     L.plba_synchronize.argtypes = [vp]
     L.plba_enable_kernel_timing.argtypes = [vp, C.c_int32]
     L.plba_kernel_times.argtypes = [vp, C.POINTER(C.c_char_p), dp, ip, C.c_int32, ip]
+    L.plba_structure_stats.argtypes = [vp, C.POINTER(C.c_int64), C.c_int32]
     for name in EXPORTED:
         f = getattr(L, name)
         if name not in ("plba_default_opts", "plba_last_error"):
@@ -192,6 +193,11 @@ class Solver:
         self._check(self.L.plba_kernel_times(self.ctx, names, _p(ms), _p(nl, C.c_int32), cap, C.byref(n)),
                     "plba_kernel_times")
         return {names[i].decode(): (float(ms[i]), int(nl[i])) for i in range(n.value)}
+
+    def structure_stats(self) -> dict:
+        st = (C.c_int64 * 8)()
+        self._check(self.L.plba_structure_stats(self.ctx, st, 8), "plba_structure_stats")
+        return dict(nf=st[0], bw=st[1], nblk=st[2], triples=st[3], edges=st[4], landmarks=st[5], banded=st[6])
 
     def synchronize(self):
         self._check(self.L.plba_synchronize(self.ctx), "plba_synchronize")
