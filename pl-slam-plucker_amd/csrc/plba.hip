@@ -37,12 +37,13 @@ namespace plba {
     } while (0)
 
 enum KernelId {
-    K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_SCHUR, K_MEMSET, K_ASSEMBLE, K_FACTOR,
-    K_POSE_UPDATE, K_LM_UPDATE, K_DECIDE, K_COMMIT, K_COUNT
+    K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_SCHUR, K_ESCHUR, K_MEMSET, K_ASSEMBLE, K_FINALIZE,
+    K_FACTOR, K_POSE_UPDATE, K_BACKSUB, K_LM_UPDATE, K_EVAL, K_DECIDE, K_COMMIT, K_COUNT
 };
 static const char *kKernelNames[K_COUNT] = {
-    "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_schur_landmark", "memset_rcs",
-    "k_rcs_assemble", "k_rcs_factor", "k_pose_update", "k_landmark_update", "k_decide", "k_commit"};
+    "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_lm_chol", "k_edge_schur", "memset_rcs",
+    "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_edge_backsub", "k_lm_solve",
+    "k_edge_eval", "k_decide", "k_commit"};
 
 }  // namespace plba
 
@@ -344,6 +345,18 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         }
         ctx->n_triples = tot;
     }
+    // chunks of <= kChunk triples, never spanning two blocks
+    std::vector<int32_t> ch_blk, ch_off, blk_ch(nblk + 1, 0);
+    for (int k = 0; k < nblk; ++k) {
+        blk_ch[k] = (int32_t)ch_blk.size();
+        for (int t = blk_off[k]; t < blk_off[k + 1]; t += kChunk) {
+            ch_blk.push_back(k);
+            ch_off.push_back(t);
+        }
+    }
+    blk_ch[nblk] = (int32_t)ch_blk.size();
+    ch_off.push_back(blk_off[nblk]);
+    const int nch = (int)ch_blk.size();
     // envelope of the lower triangle (per 6-row pose block: first pose block column)
     const int n = 6 * nf;
     const int ntiles = (n + kTile - 1) / kTile;
@@ -427,6 +440,11 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.blk_i2, blk_i2);
     UPLOAD(d.blk_off, blk_off);
     UPLOAD(d.trip, trip);
+    d.nch = nch;
+    UPLOAD(d.ch_blk, ch_blk);
+    UPLOAD(d.ch_off, ch_off);
+    UPLOAD(d.blk_ch, blk_ch);
+    ALLOC(d.ch_part, (size_t)std::max(nch, 1) * 42);
     ALLOC(d.Ad, band_mode ? 1 : (size_t)n * n);
     UPLOAD(d.first_blk, first_blk);
     ALLOC(d.Bd, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
@@ -440,7 +458,9 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.tile_last, tile_last);
     ALLOC(d.part_chi2, d.n_lin_blocks);
     ALLOC(d.part_max, nf + d.n_lm_blocks);
-    ALLOC(d.part_lm, d.n_lm_blocks);
+    ALLOC(d.part_lm, std::max(d.n_lin_blocks, d.n_lm_blocks));
+    ALLOC(d.ue, (size_t)E * 4);
+    ALLOC(d.Xplk, (size_t)n_lm * 6);
     ALLOC(d.part_lms, d.n_lm_blocks);
     ALLOC(d.part_ps, d.n_kf_blocks);
     ALLOC(d.ctrl, 1);
@@ -496,11 +516,15 @@ int lm_iteration(plba_ctx *ctx, int it) {
     LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kBlock), 0, s, d, it));
     const Ctrl &c = *ctx->h_ctrl;
     for (;;) {
-        if (d.n_lm > 0) LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_schur_landmark, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+        if (d.n_lm > 0) {
+            LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_lm_chol, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+            LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+        }
         if (d.n > 0) {
             if (!d.band_mode)
                 LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
-            LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_assemble, dim3(blocks_for(d.nblk * 64)), dim3(kBlock), 0, s, d));
+            if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_chunk, dim3(d.nch), dim3(64), 0, s, d));
+            LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
             if (d.band_mode)
                 LAUNCH(K_FACTOR, launch_band(d, band_lds_bytes(d.bw, d.nf), s));
             else
@@ -510,7 +534,11 @@ int lm_iteration(plba_ctx *ctx, int it) {
             PLBA_CHECK(hipMemcpyAsync(&d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, s));
         }
         if (d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(d.n_kf_blocks), dim3(kBlock), 0, s, d));
-        if (d.n_lm > 0) LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_landmark_update, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+        if (d.n_lm > 0) {
+            LAUNCH(K_BACKSUB, hipLaunchKernelGGL(k_edge_backsub, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+            LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+            LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+        }
         LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d, max_trials));
         int nv = std::max(d.n_lm, d.n_kf);
         LAUNCH(K_COMMIT, hipLaunchKernelGGL(k_commit, dim3(blocks_for(std::max(nv, 1))), dim3(kBlock), 0, s, d));

@@ -25,6 +25,7 @@
 namespace plba {
 
 constexpr int kBlock = 256;
+constexpr int kChunk = 128;  // Schur triples per assembly wave (2 per lane)
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
 constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window factorisation holds
 #ifndef PLBA_BAND_NT
@@ -67,6 +68,10 @@ struct Dev {
     // reduced camera system
     int32_t *blk_i1, *blk_i2, *blk_off; // [nblk], [nblk], [nblk+1]
     int32_t *trip;                      // [T][2]
+    int32_t nch;                        // triple chunks (<= kChunk triples, one block each)
+    int32_t *ch_blk, *ch_off;           // [nch], [nch+1] (triple range)
+    int32_t *blk_ch;                    // [nblk+1] chunk range of each block
+    double *ch_part;                    // [nch][42]  partial block sums (36) + b_s sums (6)
     double *Ad, *bs, *xp, *Wbuf;        // [n*n], [n], [n], [n*kTile]
     int32_t *tile_first;                // [ntiles] first nonzero column tile of each row tile
     int32_t *tile_last;                 // [ntiles] last row tile whose envelope reaches column tile K
@@ -82,7 +87,9 @@ struct Dev {
     // reductions
     double *part_chi2;                  // [n_lin_blocks]
     double *part_max;                   // [nf + n_lm_blocks]
-    double *part_lm, *part_lms;         // [n_lm_blocks]
+    double *part_lm, *part_lms;         // [n_lin_blocks] trial χ² partials, [n_lm_blocks] scale partials
+    double *ue;                         // [E][4]  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)
+    double *Xplk;                       // [n_lm][6] trial Plücker of lines (xyz of points)
     double *part_ps;                    // [n_kf_blocks]
     Ctrl *ctrl;
 };
@@ -477,6 +484,93 @@ __global__ __launch_bounds__(kBlock) void k_rcs_assemble(Dev d) {
         // block (i1,i2) row r of i1, col c of i2  -> lower position (6 i2 + c, 6 i1 + r)
         if (d.band_mode) d.Bd[((size_t)i2 * (d.bw + 1) + (i2 - i1)) * 36 + c * 6 + r] = -v;
         else d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -v;
+    }
+}
+
+// Chunked reduced-camera assembly, pass 1: one wave per chunk of <= kChunk triples of one
+// block; each lane accumulates A₁ᵀ(Z₁Z₂ᵀ)A₂ (36) and, for self-triples of a diagonal block,
+// A_eᵀ q_e (6); the wave reduces through LDS in fixed lane order (deterministic).
+__global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
+    __shared__ double red[64][43];
+    const int ch = blockIdx.x, lane = threadIdx.x;
+    const int b = d.ch_blk[ch];
+    const bool diag = d.blk_i1[b] == d.blk_i2[b];
+    double acc[42];
+#pragma unroll
+    for (int k = 0; k < 42; ++k) acc[k] = 0.0;
+    const int t0 = d.ch_off[ch], t1 = d.ch_off[ch + 1];
+#pragma unroll
+    for (int q = 0; q < kChunk / 64; ++q) {
+        const int t = t0 + lane + 64 * q;
+        if (t < t1) {
+            const int e1 = d.trip[2 * t], e2 = d.trip[2 * t + 1];
+            const double *Z1 = d.Z + (size_t)e1 * 8, *Z2 = d.Z + (size_t)e2 * 8;
+            const double *A1 = d.A + (size_t)e1 * 12, *A2 = d.A + (size_t)e2 * 12;
+            double z1[8], z2[8], a1[12], a2[12];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { z1[k] = Z1[k]; z2[k] = Z2[k]; }
+#pragma unroll
+            for (int k = 0; k < 12; ++k) { a1[k] = A1[k]; a2[k] = A2[k]; }
+            double m00 = 0, m01 = 0, m10 = 0, m11 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                m00 = fma(z1[k], z2[k], m00);
+                m01 = fma(z1[k], z2[4 + k], m01);
+                m10 = fma(z1[4 + k], z2[k], m10);
+                m11 = fma(z1[4 + k], z2[4 + k], m11);
+            }
+            double Q[12];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                Q[k] = m00 * a2[k] + m01 * a2[6 + k];
+                Q[6 + k] = m10 * a2[k] + m11 * a2[6 + k];
+            }
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) acc[r * 6 + c] += a1[r] * Q[c] + a1[6 + r] * Q[6 + c];
+            if (diag && e1 == e2) {
+                const double q0 = d.q[(size_t)e1 * 2], q1 = d.q[(size_t)e1 * 2 + 1];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) acc[36 + r] += a1[r] * q0 + a1[6 + r] * q1;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 42; ++k) red[lane][k] = acc[k];
+    __syncthreads();
+    if (lane < 42) {
+        double sacc = 0.0;
+        for (int l = 0; l < 64; ++l) sacc += red[l][lane];
+        d.ch_part[(size_t)ch * 42 + lane] = sacc;
+    }
+}
+
+// pass 2: per block entry, sum its chunks in order, add Hpp + λI (diagonal), write the band /
+// dense matrix and b_s = b_p - Σ A_eᵀ q_e.
+__global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
+    const int gid = blockIdx.x * kBlock + threadIdx.x;
+    const int b = gid / 42, e = gid % 42;
+    if (b >= d.nblk) return;
+    const int i1 = d.blk_i1[b], i2 = d.blk_i2[b];
+    const bool diag = i1 == i2;
+    if (e >= 36 && !diag) return;
+    double sacc = 0.0;
+    for (int c = d.blk_ch[b]; c < d.blk_ch[b + 1]; ++c) sacc += d.ch_part[(size_t)c * 42 + e];
+    const int n = d.n;
+    if (e >= 36) {
+        d.bs[6 * i1 + (e - 36)] = d.bp[(size_t)i1 * 6 + (e - 36)] - sacc;
+        return;
+    }
+    const int r = e / 6, c = e % 6;
+    if (diag) {
+        double h = d.Hpp[(size_t)i1 * 36 + e] - sacc;
+        if (r == c) h += d.ctrl->lambda;
+        if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
+        else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
+    } else {
+        if (d.band_mode) d.Bd[((size_t)i2 * (d.bw + 1) + (i2 - i1)) * 36 + c * 6 + r] = -sacc;
+        else d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -sacc;
     }
 }
 
@@ -1078,11 +1172,213 @@ __global__ __launch_bounds__(kBlock) void k_landmark_update(Dev d) {
     }
 }
 
+// ---------------------------------------------------------------- edge-parallel trial path
+// per landmark: (Hll + λI) = L Lᵀ, g = L⁻¹ b_l
+__global__ __launch_bounds__(kBlock) void k_lm_chol(Dev d) {
+    const int l = blockIdx.x * kBlock + threadIdx.x;
+    if (l >= d.n_lm) return;
+    const double lam = d.ctrl->lambda;
+    const int DIM = is_point_lm(d, l) ? 3 : 4;
+    double H[10], L[10], g[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 10; ++k) { H[k] = d.Hll[(size_t)l * 10 + k]; L[k] = 0.0; }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j < DIM) {
+            double sj = H[pk(j, j)] + lam;
+#pragma unroll
+            for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
+            const double djj = sqrt(sj);
+            L[pk(j, j)] = djj;
+#pragma unroll
+            for (int i = j + 1; i < 4; ++i) {
+                if (i < DIM) {
+                    double t = H[pk(i, j)];
+#pragma unroll
+                    for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
+                    L[pk(i, j)] = t / djj;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i < DIM) {
+            double t = d.bl[(size_t)l * 4 + i];
+#pragma unroll
+            for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * g[p];
+            g[i] = t / L[pk(i, i)];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) d.Lc[(size_t)l * 10 + k] = L[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d.gv[(size_t)l * 4 + k] = g[k];
+}
+// per edge: Z_e = B_e L⁻ᵀ (rows solved with L), q_e = Z_e g
+__global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= d.E) return;
+    const int l = d.e_lm[e];
+    const int DIM = e < d.Ep ? 3 : 4;
+    double L[10], g[4], B[8];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) L[k] = d.Lc[(size_t)l * 10 + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] = d.gv[(size_t)l * 4 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) B[k] = d.B[(size_t)e * 8 + k];
+    double z[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < DIM) {
+                double t = B[r * 4 + i];
+#pragma unroll
+                for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * z[r][p];
+                z[r][i] = t / L[pk(i, i)];
+            }
+        }
+    double *Z = d.Z + (size_t)e * 8;
+    double q0 = 0, q1 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        Z[i] = z[0][i];
+        Z[4 + i] = z[1][i];
+        q0 += z[0][i] * g[i];
+        q1 += z[1][i] * g[i];
+    }
+    d.q[(size_t)e * 2 + 0] = q0;
+    d.q[(size_t)e * 2 + 1] = q1;
+}
+// per edge: u_e = B_eᵀ (A_e x_p)
+__global__ __launch_bounds__(kBlock) void k_edge_backsub(Dev d) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= d.E || !d.ctrl->solve_ok) return;
+    const int h = d.e_hidx[e];
+    double u[4] = {0, 0, 0, 0};
+    if (h >= 0) {
+        const double *A = d.A + (size_t)e * 12;
+        const double *B = d.B + (size_t)e * 8;
+        double ax0 = 0, ax1 = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const double xk = d.xp[6 * h + k];
+            ax0 += A[k] * xk;
+            ax1 += A[6 + k] * xk;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u[i] = B[i] * ax0 + B[4 + i] * ax1;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d.ue[(size_t)e * 4 + i] = u[i];
+}
+// per landmark: x_l = L⁻ᵀ L⁻¹ (b_l - Σ u_e), oplus into the trial state, scale partial
+__global__ __launch_bounds__(kBlock) void k_lm_solve(Dev d) {
+    __shared__ double sh[kBlock / 64];
+    const int l = blockIdx.x * kBlock + threadIdx.x;
+    double sc = 0.0;
+    if (l < d.n_lm) {
+        const double *Xc = d.X_cur + (size_t)l * 4;
+        double *Xt = d.X_trial + (size_t)l * 4;
+        if (d.lm_active[l]) {
+            const bool pt = is_point_lm(d, l);
+            const int DIM = pt ? 3 : 4;
+            const double lam = d.ctrl->lambda;
+            double x[4] = {0, 0, 0, 0};
+            if (d.ctrl->solve_ok) {
+                double r[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) r[i] = d.bl[(size_t)l * 4 + i];
+                for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) r[i] -= d.ue[(size_t)e * 4 + i];
+                double L[10], y[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < 10; ++k) L[k] = d.Lc[(size_t)l * 10 + k];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (i < DIM) {
+                        double t = r[i];
+#pragma unroll
+                        for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * y[p];
+                        y[i] = t / L[pk(i, i)];
+                    }
+#pragma unroll
+                for (int i = 3; i >= 0; --i)
+                    if (i < DIM) {
+                        double t = y[i];
+#pragma unroll
+                        for (int p = i + 1; p < 4; ++p)
+                            if (p < DIM) t -= L[pk(p, i)] * x[p];
+                        x[i] = t / L[pk(i, i)];
+                    }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) d.xl[(size_t)l * 4 + i] = x[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = d.xl[(size_t)l * 4 + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (i < DIM) sc += x[i] * (lam * x[i] + d.bl[(size_t)l * 4 + i]);
+            double X[4];
+            if (pt) {
+                X[0] = Xc[0] + x[0]; X[1] = Xc[1] + x[1]; X[2] = Xc[2] + x[2]; X[3] = 0.0;
+            } else {
+                const double in[4] = {Xc[0], Xc[1], Xc[2], Xc[3]};
+                orth_oplus(in, x, X);
+                double Lp[6];
+                orth_to_pluker(X, Lp);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) d.Xplk[(size_t)l * 6 + k] = Lp[k];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Xt[i] = X[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
+        }
+    }
+    const double s2 = block_sum<kBlock>(sc, sh);
+    if (threadIdx.x == 0) d.part_lms[blockIdx.x] = s2;
+}
+// per edge: χ² at the trial state (last-evaluated semantics), robust partial sums
+__global__ __launch_bounds__(kBlock) void k_edge_eval(Dev d) {
+    __shared__ double sh[kBlock / 64];
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    double chi = 0.0;
+    if (e < d.E && d.e_active[e]) {
+        const int l = d.e_lm[e];
+        const double *T = d.T_trial + (size_t)d.e_kf[e] * 12;
+        const double *obs = d.e_obs + (size_t)e * 4;
+        double err[2], delta;
+        if (e < d.Ep) {
+            double z;
+            point_error(T, d.X_trial + (size_t)l * 4, obs, d.cam, err, z);
+            delta = d.huber_pt;
+        } else {
+            line_error(T, d.Xplk + (size_t)l * 6, obs, d.cam, err);
+            delta = d.huber_ln;
+        }
+        const double info = d.e_info[e];
+        const double c2 = err[0] * (info * err[0]) + err[1] * (info * err[1]);
+        d.chi2_last[e] = c2;
+        double rho0 = c2, rho1;
+        if (d.robust) huber(c2, delta, rho0, rho1);
+        chi = rho0;
+    }
+    const double s1 = block_sum<kBlock>(chi, sh);
+    if (threadIdx.x == 0) d.part_lm[blockIdx.x] = s1;
+}
+
 // OptimizationAlgorithmLevenberg trial decision
 __global__ __launch_bounds__(kBlock) void k_decide(Dev d, int max_trials) {
     __shared__ double sh[kBlock / 64];
     double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) { a += d.part_lm[i]; b += d.part_lms[i]; }
+    for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
+    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) b += d.part_lms[i];
     for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];
     const double tempChi0 = block_sum<kBlock>(a, sh);
     const double scale0 = block_sum<kBlock>(b, sh);
