@@ -37,11 +37,12 @@ namespace plba {
     } while (0)
 
 enum KernelId {
-    K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_SCHUR, K_ESCHUR, K_MEMSET, K_ASSEMBLE, K_FINALIZE,
-    K_FACTOR, K_POSE_UPDATE, K_BACKSUB, K_LM_UPDATE, K_EVAL, K_DECIDE, K_COMMIT, K_COUNT
+    K_SWITCH, K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_SCHUR, K_ESCHUR, K_MEMSET, K_ASSEMBLE,
+    K_FINALIZE, K_FACTOR, K_POSE_UPDATE, K_BACKSUB, K_LM_UPDATE, K_EVAL, K_DECIDE, K_COMMIT, K_COUNT
 };
 static const char *kKernelNames[K_COUNT] = {
-    "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_lm_chol", "k_edge_schur", "memset_rcs",
+    "k_switch(4)", "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_lm_chol", "k_edge_schur",
+    "memset_rcs",
     "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_edge_backsub", "k_lm_solve",
     "k_edge_eval", "k_decide", "k_commit"};
 
@@ -68,6 +69,11 @@ struct plba_ctx {
     std::vector<plba_iter_trace> trace;
     int stage = 0;
     size_t n_triples = 0;
+    // captured step graph (one LM trial + guarded iteration / stage-switch work)
+    hipGraph_t step_graph = nullptr;
+    hipGraphExec_t step_exec = nullptr;
+    int last_steps = 16;     // steps the previous schedule needed (first batch size)
+    int steps_launched = 0;
     // kernel timing (optional)
     bool timing = false;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;
@@ -86,6 +92,10 @@ struct plba_ctx {
         if (opts.verbose) fprintf(stderr, "[plba] %s\n", buf);
     }
     void free_all() {
+        if (step_exec) (void)hipGraphExecDestroy(step_exec);
+        if (step_graph) (void)hipGraphDestroy(step_graph);
+        step_exec = nullptr;
+        step_graph = nullptr;
         for (void *p : allocs) (void)hipFree(p);
         allocs.clear();
         d = Dev{};
@@ -381,7 +391,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.band_mode = band_mode ? 1 : 0;
     d.ring = band_ring(bw, nf);
     d.corrected = ctx->opts.corrected_line_jacobian;
-    d.robust = 1;
     d.cam = Cam{g->fx, g->fy, g->cx, g->cy};
     d.huber_pt = g->huber_pt;
     d.huber_ln = g->huber_ln;
@@ -464,6 +473,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_lms, d.n_lm_blocks);
     ALLOC(d.part_ps, d.n_kf_blocks);
     ALLOC(d.ctrl, 1);
+    ALLOC(d.trace, kTraceCap);
     ALLOC(ctx->d_depth, Ep);
 #ifdef PLBA_STAMPS
     ALLOC(d.stamps, 16 * 8);
@@ -484,18 +494,61 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     return PLBA_OK;
 }
 
-int do_initialize(plba_ctx *ctx, int level) {
+// One "step": [stage switch] -> [iteration: linearise + reductions + λ init] -> one damped
+// trial -> decide -> commit. Every kernel is guarded by the device control block, so a fixed
+// sequence can be captured once and replayed; steps after the schedule finished are no-ops.
+int launch_step(plba_ctx *ctx) {
     Dev &d = ctx->d;
-    d.robust = ctx->robust;
-    if (d.n_lm) PLBA_CHECK(hipMemsetAsync(d.lm_active, 0, d.n_lm, ctx->stream));
-    if (d.n_kf) PLBA_CHECK(hipMemsetAsync(d.kf_active, 0, d.n_kf, ctx->stream));
-    if (d.E > 0) {
-        hipLaunchKernelGGL(k_activate_edges, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d, level);
-        hipLaunchKernelGGL(k_activate_vertices, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d);
+    hipStream_t s = ctx->stream;
+    const int nv = std::max(std::max(d.n_lm, d.n_kf), 1);
+    LAUNCH(K_SWITCH, {
+        if (d.E > 0) hipLaunchKernelGGL(k_switch_classify, dim3(blocks_for(d.E)), dim3(kBlock), 0, s, d, 5.991);
+        hipLaunchKernelGGL(k_switch_clear, dim3(blocks_for(nv)), dim3(kBlock), 0, s, d);
+        if (d.E > 0) hipLaunchKernelGGL(k_switch_activate, dim3(blocks_for(d.E)), dim3(kBlock), 0, s, d);
+        hipLaunchKernelGGL(k_switch_finish, dim3(1), dim3(64), 0, s, d);
+    });
+    if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+    if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kBlock), 0, s, d));
+    if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+    LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kBlock), 0, s, d));
+    if (d.n_lm > 0) {
+        LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_lm_chol, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+        LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }
-    PLBA_CHECK(hipGetLastError());
-    ctx->level = level;
-    ctx->initialized = true;
+    if (d.n > 0) {
+        if (!d.band_mode) LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
+        if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_chunk, dim3(d.nch), dim3(64), 0, s, d));
+        LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
+        if (d.band_mode) LAUNCH(K_FACTOR, launch_band(d, band_lds_bytes(d.bw, d.nf), s));
+        else LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
+    }
+    if (d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(d.n_kf_blocks), dim3(kBlock), 0, s, d));
+    if (d.n_lm > 0) {
+        LAUNCH(K_BACKSUB, hipLaunchKernelGGL(k_edge_backsub, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+        LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+        LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+    }
+    LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d));
+    LAUNCH(K_COMMIT, hipLaunchKernelGGL(k_commit, dim3(blocks_for(nv)), dim3(kBlock), 0, s, d));
+    return PLBA_OK;
+}
+
+int capture_step(plba_ctx *ctx) {
+    if (ctx->step_exec) return PLBA_OK;
+    const bool t = ctx->timing;
+    ctx->timing = false;
+    PLBA_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    int rc = launch_step(ctx);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    ctx->timing = t;
+    if (rc) return rc;
+    if (e != hipSuccess) {
+        ctx->set_error("graph capture failed: %s", hipGetErrorString(e));
+        return PLBA_E_DEVICE;
+    }
+    ctx->step_graph = g;
+    PLBA_CHECK(hipGraphInstantiate(&ctx->step_exec, g, nullptr, nullptr, 0));
     return PLBA_OK;
 }
 
@@ -505,85 +558,74 @@ int read_ctrl(plba_ctx *ctx) {
     return PLBA_OK;
 }
 
-// OptimizationAlgorithmLevenberg::solve(iteration). Returns 0 OK, 1 Terminate, <0 error.
-int lm_iteration(plba_ctx *ctx, int it) {
+// Run a schedule of 1 or 2 optimize() calls entirely on the device: replay the step graph in
+// batches, polling the control block once per batch.
+int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     Dev &d = ctx->d;
-    hipStream_t s = ctx->stream;
-    const int max_trials = ctx->opts.max_trials;
-    if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
-    if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kBlock), 0, s, d));
-    if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
-    LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kBlock), 0, s, d, it));
-    const Ctrl &c = *ctx->h_ctrl;
+    *ctx->h_ctrl = init;
+    PLBA_CHECK(hipMemcpyAsync(d.ctrl, ctx->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, ctx->stream));
+    const bool use_graph = !ctx->timing;
+    if (use_graph) {
+        int rc = capture_step(ctx);
+        if (rc) return rc;
+    }
+    int launched = 0;
+    int batch = std::max(4, ctx->last_steps);
+    const int max_steps = init.n_stages * 10 * (init.max_iters[0] + init.max_iters[1] + 2) + 8;
     for (;;) {
-        if (d.n_lm > 0) {
-            LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_lm_chol, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
-            LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+        for (int b = 0; b < batch; ++b) {
+            if (use_graph) PLBA_CHECK(hipGraphLaunch(ctx->step_exec, ctx->stream));
+            else {
+                int rc = launch_step(ctx);
+                if (rc) return rc;
+            }
         }
-        if (d.n > 0) {
-            if (!d.band_mode)
-                LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
-            if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_chunk, dim3(d.nch), dim3(64), 0, s, d));
-            LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
-            if (d.band_mode)
-                LAUNCH(K_FACTOR, launch_band(d, band_lds_bytes(d.bw, d.nf), s));
-            else
-                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
-        } else {
-            int one = 1;
-            PLBA_CHECK(hipMemcpyAsync(&d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, s));
-        }
-        if (d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(d.n_kf_blocks), dim3(kBlock), 0, s, d));
-        if (d.n_lm > 0) {
-            LAUNCH(K_BACKSUB, hipLaunchKernelGGL(k_edge_backsub, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
-            LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
-            LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
-        }
-        LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d, max_trials));
-        int nv = std::max(d.n_lm, d.n_kf);
-        LAUNCH(K_COMMIT, hipLaunchKernelGGL(k_commit, dim3(blocks_for(std::max(nv, 1))), dim3(kBlock), 0, s, d));
+        launched += batch;
         int rc = read_ctrl(ctx);
         if (rc) return rc;
-        if (c.broke) break;
-        if (!(c.rho < 0 && c.qmax < max_trials)) break;
+        if (ctx->h_ctrl->all_done) break;
+        if (launched >= max_steps) {
+            ctx->set_error("LM schedule did not terminate after %d steps", launched);
+            return PLBA_E_STATE;
+        }
+        // steps still needed: at least one per remaining trial; keep batches small near the end
+        batch = 4;
     }
-    int result = 0;
-    if (c.qmax == max_trials || c.rho == 0 || !std::isfinite(c.lambda)) result = 1;
-    ctx->trace.push_back(plba_iter_trace{ctx->stage, it, c.qmax, result, c.chi2_start, c.currentChi, c.lambda_start,
-                                         c.lambda});
-    if (ctx->opts.verbose)
-        fprintf(stderr, "[plba] stage %d it %d chi2 %.9g -> %.9g lambda %.6g trials %d\n", ctx->stage, it,
-                c.chi2_start, c.currentChi, c.lambda, c.qmax);
-    return result;
+    ctx->steps_launched = launched;
+    ctx->last_steps = std::max(4, ctx->h_ctrl->steps + 1);
+    // per-iteration trace written by k_decide
+    const int nt = std::min(ctx->h_ctrl->ntrace, kTraceCap);
+    std::vector<plba_iter_trace> tr(nt);
+    if (nt) PLBA_CHECK(hipMemcpy(tr.data(), d.trace, sizeof(plba_iter_trace) * nt, hipMemcpyDeviceToHost));
+    ctx->trace.insert(ctx->trace.end(), tr.begin(), tr.end());
+    return PLBA_OK;
+}
+
+Ctrl schedule_init(plba_ctx *ctx, int n_stages) {
+    Ctrl c{};
+    c.stage = -1;
+    c.n_stages = n_stages;
+    c.switch_pending = 1;
+    c.solve_ok = 1;
+    c.max_trials = ctx->opts.max_trials;
+    return c;
 }
 
 int do_optimize(plba_ctx *ctx, int iterations, int32_t *iters_done, double *final_chi2) {
-    Dev &d = ctx->d;
-    // g2o returns -1 without iterating when no vertex is free & active (_ivMap empty)
-    std::vector<uint8_t> lm_act(d.n_lm), kf_act(d.n_kf);
-    bool any = false;
-    {
-        if (d.n_lm) PLBA_CHECK(hipMemcpyAsync(lm_act.data(), d.lm_active, d.n_lm, hipMemcpyDeviceToHost, ctx->stream));
-        if (d.n_kf) PLBA_CHECK(hipMemcpyAsync(kf_act.data(), d.kf_active, d.n_kf, hipMemcpyDeviceToHost, ctx->stream));
-        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
-        for (auto a : lm_act) any |= a != 0;
-        for (auto a : kf_act) any |= a != 0;
-    }
-    if (!any) {
-        if (iters_done) *iters_done = -1;
+    Ctrl c = schedule_init(ctx, 1);
+    c.max_iters[0] = iterations;
+    c.stage_robust[0] = ctx->robust;
+    c.stage_level[0] = ctx->level;
+    c.stage_classify[0] = 0;
+    if (iterations <= 0) {
+        if (iters_done) *iters_done = 0;
         if (final_chi2) *final_chi2 = 0.0;
         return PLBA_OK;
     }
-    d.robust = ctx->robust;
-    int done = 0;
-    for (int it = 0; it < iterations; ++it) {
-        int r = lm_iteration(ctx, it);
-        if (r < 0) return r;
-        ++done;
-        if (r != 0) break;
-    }
-    if (iters_done) *iters_done = done;
-    if (final_chi2) *final_chi2 = ctx->h_ctrl->currentChi;
+    int rc = run_schedule(ctx, c);
+    if (rc) return rc;
+    if (iters_done) *iters_done = ctx->h_ctrl->iters_done[0];
+    if (final_chi2) *final_chi2 = ctx->h_ctrl->chi2_final[0];
     return PLBA_OK;
 }
 
@@ -688,24 +730,23 @@ int plba_set_edge_levels(plba_ctx *ctx, const uint8_t *ept_level, const uint8_t 
 int plba_set_robust(plba_ctx *ctx, int32_t robust) {
     if (!ctx) return PLBA_E_INVALID;
     ctx->robust = robust ? 1 : 0;
-    ctx->d.robust = ctx->robust;
     return PLBA_OK;
 }
 
 int plba_initialize_optimization(plba_ctx *ctx, int32_t level) {
     if (!ctx) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    (void)hipSetDevice(ctx->opts.device);
-    return do_initialize(ctx, level);
+    ctx->level = level;  // activation runs on the device at the start of the next optimize()
+    ctx->initialized = true;
+    return PLBA_OK;
 }
 
 int plba_optimize(plba_ctx *ctx, int32_t iterations, int32_t *iters_done, double *final_chi2) {
     if (!ctx) return PLBA_E_INVALID;
     if (!ctx->uploaded || !ctx->initialized) return PLBA_E_STATE;
     (void)hipSetDevice(ctx->opts.device);
-    int rc = do_optimize(ctx, iterations, iters_done, final_chi2);
-    ctx->stage++;
-    return rc;
+    ctx->trace.clear();
+    return do_optimize(ctx, iterations, iters_done, final_chi2);
 }
 
 int plba_refresh_edge_errors(plba_ctx *ctx, int32_t level) {
@@ -768,31 +809,29 @@ int plba_lba_plucker(plba_ctx *ctx, plba_result *res) {
     for (int k = 0; k < K_COUNT; ++k) { ctx->k_ms[k] = 0; ctx->k_n[k] = 0; }
     auto t0 = std::chrono::steady_clock::now();
     int rc;
-    int it1 = 0, it2 = 0;
-    double chi1 = 0, chi2 = 0;
-    // stage 1: all edges level 0, Huber on
-    ctx->robust = 1;
-    ctx->stage = 0;
-    if ((rc = do_initialize(ctx, 0))) return rc;
-    if ((rc = do_optimize(ctx, 5, &it1, &chi1))) return rc;
-    // classification: chi2 > 5.991 || depth <= 0 -> level 1; kernels removed
-    if (d.E > 0) hipLaunchKernelGGL(k_classify, dim3(blocks_for(d.E)), dim3(kBlock), 0, ctx->stream, d, 5.991);
-    PLBA_CHECK(hipGetLastError());
-    ctx->robust = 0;
-    // stage 2
-    ctx->stage = 1;
-    if ((rc = do_initialize(ctx, 0))) return rc;
-    if ((rc = do_optimize(ctx, 10, &it2, &chi2))) return rc;
+    // stage 1: level 0, Huber; classification; stage 2: level 0, no kernel
+    Ctrl c = schedule_init(ctx, 2);
+    c.max_iters[0] = 5;
+    c.max_iters[1] = 10;
+    c.stage_robust[0] = 1;
+    c.stage_robust[1] = 0;
+    c.stage_level[0] = 0;
+    c.stage_level[1] = 0;
+    c.stage_classify[0] = 0;
+    c.stage_classify[1] = 1;
+    if ((rc = run_schedule(ctx, c))) return rc;
     // computeError() on the level-1 edges at the final state
     if ((rc = launch_edges(ctx, k_refresh, 1))) return rc;
     PLBA_CHECK(hipStreamSynchronize(ctx->stream));
     auto t1 = std::chrono::steady_clock::now();
     if ((rc = collect_timing(ctx))) return rc;
+    ctx->robust = 0;
+    ctx->level = 0;
     if (res) {
-        res->iters[0] = it1;
-        res->iters[1] = it2;
-        res->chi2[0] = chi1;
-        res->chi2[1] = chi2;
+        res->iters[0] = ctx->h_ctrl->iters_done[0];
+        res->iters[1] = ctx->h_ctrl->iters_done[1];
+        res->chi2[0] = ctx->h_ctrl->chi2_final[0];
+        res->chi2[1] = ctx->h_ctrl->chi2_final[1];
         res->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if ((rc = plba_download(ctx, res->kf_Tcw, res->pt_xyz, res->ln_orth))) return rc;
         if (res->ept_chi2 || res->ept_depth_ok || res->eln_chi2)

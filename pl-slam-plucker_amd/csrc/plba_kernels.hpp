@@ -6,6 +6,7 @@
 //   k_pose_reduce      pose-parallel deterministic segmented sum: Hpp, b_p
 //   k_landmark_reduce  landmark-parallel: Hll, b_l; max|diag| partials
 //   k_iter_init        χ²_cur, λ init (τ·max|H_jj|, iteration 0)
+// Stage switch (initializeOptimization): k_switch_classify / _clear / _activate / _finish.
 // Per damped trial:
 //   k_schur_landmark   (Hll+λI) = LLᵀ per landmark; Z_e = B_e L⁻ᵀ, q_e = Z_e L⁻¹ b_l
 //   k_rcs_assemble     one wave per reduced-camera block: Hpp+λI − Σ A₁ᵀ(Z₁Z₂ᵀ)A₂ ; b_s
@@ -20,12 +21,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/plba.h"
 #include "plba_math.hpp"
 
 namespace plba {
 
 constexpr int kBlock = 256;
 constexpr int kChunk = 128;  // Schur triples per assembly wave (2 per lane)
+constexpr int kTraceCap = 64;
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
 constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window factorisation holds
 #ifndef PLBA_BAND_NT
@@ -33,17 +36,26 @@ constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window 
 #endif
 constexpr int kBandNT = PLBA_BAND_NT; // threads of the banded factorisation workgroup
 
+// Device-resident LM control block: the g2o optimize()/solve() loop runs as a state machine
+// advanced by k_decide, so the host only replays a captured "step" graph and polls this block.
 struct Ctrl {
     double lambda, ni, currentChi, tempChi, rho, scale, maxdiag;
     double chi2_start, lambda_start;
+    double chi2_final[2];
     int32_t qmax, accept, solve_ok, broke;
-    int32_t pad[4];
+    int32_t stage, n_stages, iter, need_iter;        // schedule position
+    int32_t all_done, switch_pending, robust, level;
+    int32_t max_iters[2], iters_done[2];
+    int32_t stage_robust[2], stage_level[2], stage_classify[2];
+    int32_t max_trials, ntrace, any_active, commit_pending;
+    int32_t steps;                                     // step graphs that did work (diagnostic)
+    int32_t pad[3];
 };
 
 // All device pointers of one window (passed by value to every kernel).
 struct Dev {
     int32_t n_kf, n_pt, n_ln, n_lm, Ep, El, E, nf, n;
-    int32_t corrected, robust, n_lin_blocks, n_lm_blocks, n_kf_blocks, nblk, ntiles;
+    int32_t corrected, n_lin_blocks, n_lm_blocks, n_kf_blocks, nblk, ntiles;
     Cam cam;
     double huber_pt, huber_ln, tau;
     // state
@@ -92,6 +104,7 @@ struct Dev {
     double *Xplk;                       // [n_lm][6] trial Plücker of lines (xyz of points)
     double *part_ps;                    // [n_kf_blocks]
     Ctrl *ctrl;
+    plba_iter_trace *trace;             // [kTraceCap] per-iteration records written by k_decide
 };
 
 // ---------------------------------------------------------------- block reductions
@@ -151,22 +164,19 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// ---------------------------------------------------------------- activation
-__global__ void k_activate_edges(Dev d, int level) {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < d.E) d.e_active[e] = (d.e_level[e] == level) ? 1 : 0;
-}
-// vertices are active iff they have an active edge (writes of the constant 1 only: race-free)
-__global__ void k_activate_vertices(Dev d) {
-    int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < d.E && d.e_active[e]) {
-        d.lm_active[d.e_lm[e]] = 1;
-        d.kf_active[d.e_kf[e]] = 1;
-    }
-}
-
 // ---------------------------------------------------------------- linearisation
+#define ITER_GUARD                                   \
+    {                                                \
+        const Ctrl *cg = d.ctrl;                     \
+        if (cg->all_done || !cg->need_iter) return;  \
+    }
+#define TRIAL_GUARD                \
+    {                              \
+        if (d.ctrl->all_done) return; \
+    }
+
 __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
+    ITER_GUARD
     __shared__ double sh[kBlock / 64];
     const int e = blockIdx.x * kBlock + threadIdx.x;
     double rc = 0.0;
@@ -196,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
             const double chi = err[0] * (info * err[0]) + err[1] * (info * err[1]);
             d.chi2_last[e] = chi;
             double rho0 = chi, rho1 = 1.0;
-            if (d.robust) huber(chi, delta, rho0, rho1);
+            if (d.ctrl->robust) huber(chi, delta, rho0, rho1);
             rc = rho0;
             const double s = sqrt(rho1 * info);
             const bool pose_free = d.e_hidx[e] >= 0;
@@ -220,6 +230,7 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
 
 // one workgroup per free pose: Hpp = Σ AᵀA, b_p = Σ Aᵀc (deterministic)
 __global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
+    ITER_GUARD
     const int h = blockIdx.x;
     double acc[27];
 #pragma unroll
@@ -274,6 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
 __device__ __forceinline__ constexpr int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
 __global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
+    ITER_GUARD
     __shared__ double sh[kBlock / 64];
     const int l = blockIdx.x * kBlock + threadIdx.x;
     double mx = 0.0;
@@ -306,7 +318,8 @@ __global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
     if (threadIdx.x == 0) d.part_max[d.nf + blockIdx.x] = m;
 }
 
-__global__ __launch_bounds__(kBlock) void k_iter_init(Dev d, int iteration) {
+__global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
+    ITER_GUARD
     __shared__ double sh[kBlock / 64];
     double s = 0.0;
     for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) s += d.part_chi2[i];
@@ -318,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_iter_init(Dev d, int iteration) {
         Ctrl *c = d.ctrl;
         c->currentChi = chi;
         c->chi2_start = chi;
-        if (iteration == 0) {
+        if (c->iter == 0) {  // computeLambdaInit: τ·max|H_jj|, ν = 2
             c->maxdiag = mx;
             c->lambda = d.tau * mx;
             c->ni = 2.0;
@@ -328,169 +341,16 @@ __global__ __launch_bounds__(kBlock) void k_iter_init(Dev d, int iteration) {
         c->accept = 0;
         c->rho = 0.0;
         c->broke = 0;
+        c->need_iter = 0;
     }
-}
-
-// ---------------------------------------------------------------- Schur, per landmark
-template <int DIM>
-__device__ __forceinline__ void schur_landmark(const Dev &d, int l, double lam) {
-    double H[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) H[k] = d.Hll[(size_t)l * 10 + k];
-    // Cholesky of D = Hll + λI (DIM x DIM), packed lower
-    double L[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) L[k] = 0.0;
-#pragma unroll
-    for (int j = 0; j < DIM; ++j) {
-        double s = H[pk(j, j)] + lam;
-#pragma unroll
-        for (int p = 0; p < j; ++p) s -= L[pk(j, p)] * L[pk(j, p)];
-        const double djj = sqrt(s);
-        L[pk(j, j)] = djj;
-#pragma unroll
-        for (int i = j + 1; i < DIM; ++i) {
-            double t = H[pk(i, j)];
-#pragma unroll
-            for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
-            L[pk(i, j)] = t / djj;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 10; ++k) d.Lc[(size_t)l * 10 + k] = L[k];
-    // g = L^-1 b_l
-    double g[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < DIM; ++i) {
-        double t = d.bl[(size_t)l * 4 + i];
-#pragma unroll
-        for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * g[p];
-        g[i] = t / L[pk(i, i)];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) d.gv[(size_t)l * 4 + k] = g[k];
-    for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
-        const double *B = d.B + (size_t)e * 8;
-        double z[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int i = 0; i < DIM; ++i) {
-                double t = B[r * 4 + i];
-#pragma unroll
-                for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * z[r][p];
-                z[r][i] = t / L[pk(i, i)];
-            }
-        double *Z = d.Z + (size_t)e * 8;
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Z[r * 4 + i] = z[r][i];
-        double q0 = 0, q1 = 0;
-#pragma unroll
-        for (int i = 0; i < DIM; ++i) { q0 += z[0][i] * g[i]; q1 += z[1][i] * g[i]; }
-        d.q[(size_t)e * 2 + 0] = q0;
-        d.q[(size_t)e * 2 + 1] = q1;
-    }
-}
-__global__ __launch_bounds__(kBlock) void k_schur_landmark(Dev d) {
-    const int l = blockIdx.x * kBlock + threadIdx.x;
-    if (l >= d.n_lm) return;
-    const double lam = d.ctrl->lambda;
-    if (is_point_lm(d, l)) schur_landmark<3>(d, l, lam);
-    else schur_landmark<4>(d, l, lam);
 }
 
 // ---------------------------------------------------------------- reduced camera system
-// one wave per block (i1 <= i2): H = [i1==i2](Hpp + λI) − Σ_triples A₁ᵀ (Z₁ Z₂ᵀ) A₂
-__global__ __launch_bounds__(kBlock) void k_rcs_assemble(Dev d) {
-    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (wave >= d.nblk) return;
-    const int i1 = d.blk_i1[wave], i2 = d.blk_i2[wave];
-    double acc[36];
-#pragma unroll
-    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
-    for (int t = d.blk_off[wave] + lane; t < d.blk_off[wave + 1]; t += 64) {
-        const int e1 = d.trip[2 * t], e2 = d.trip[2 * t + 1];
-        const double *Z1 = d.Z + (size_t)e1 * 8, *Z2 = d.Z + (size_t)e2 * 8;
-        const double *A1 = d.A + (size_t)e1 * 12, *A2 = d.A + (size_t)e2 * 12;
-        double z1[8], z2[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { z1[k] = Z1[k]; z2[k] = Z2[k]; }
-        double m00 = 0, m01 = 0, m10 = 0, m11 = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            m00 += z1[k] * z2[k];
-            m01 += z1[k] * z2[4 + k];
-            m10 += z1[4 + k] * z2[k];
-            m11 += z1[4 + k] * z2[4 + k];
-        }
-        double a2[12], Q[12];
-#pragma unroll
-        for (int k = 0; k < 12; ++k) a2[k] = A2[k];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            Q[k] = m00 * a2[k] + m01 * a2[6 + k];
-            Q[6 + k] = m10 * a2[k] + m11 * a2[6 + k];
-        }
-        double a1[12];
-#pragma unroll
-        for (int k = 0; k < 12; ++k) a1[k] = A1[k];
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = 0; c < 6; ++c) acc[r * 6 + c] += a1[r] * Q[c] + a1[6 + r] * Q[6 + c];
-    }
-#pragma unroll
-    for (int k = 0; k < 36; ++k) acc[k] = wave_sum(acc[k]);
-    const int n = d.n;
-    const double lam = d.ctrl->lambda;
-    if (i1 == i2) {
-        // b_s = b_p − Σ_{e at pose} A_eᵀ q_e
-        double bacc[6] = {0, 0, 0, 0, 0, 0};
-        for (int p = d.pe_off[i1] + lane; p < d.pe_off[i1 + 1]; p += 64) {
-            const int e = d.pe_list[p];
-            const double *A = d.A + (size_t)e * 12;
-            const double q0 = d.q[(size_t)e * 2], q1 = d.q[(size_t)e * 2 + 1];
-#pragma unroll
-            for (int r = 0; r < 6; ++r) bacc[r] += A[r] * q0 + A[6 + r] * q1;
-        }
-#pragma unroll
-        for (int r = 0; r < 6; ++r) bacc[r] = wave_sum(bacc[r]);
-        if (lane < 36) {
-            const int r = lane / 6, c = lane % 6;
-            double v;
-            // select acc[lane] with a static index (avoid scratch)
-            v = 0.0;
-#pragma unroll
-            for (int k = 0; k < 36; ++k) v = (k == lane) ? acc[k] : v;
-            double h = d.Hpp[(size_t)i1 * 36 + lane] - v;
-            if (r == c) h += lam;
-            if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + lane] = h;
-            else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
-        }
-        if (lane < 6) {
-            double v = 0.0;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) v = (k == lane) ? bacc[k] : v;
-            d.bs[6 * i1 + lane] = d.bp[(size_t)i1 * 6 + lane] - v;
-        }
-    } else if (lane < 36) {
-        const int r = lane / 6, c = lane % 6;
-        double v = 0.0;
-#pragma unroll
-        for (int k = 0; k < 36; ++k) v = (k == lane) ? acc[k] : v;
-        // block (i1,i2) row r of i1, col c of i2  -> lower position (6 i2 + c, 6 i1 + r)
-        if (d.band_mode) d.Bd[((size_t)i2 * (d.bw + 1) + (i2 - i1)) * 36 + c * 6 + r] = -v;
-        else d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -v;
-    }
-}
-
 // Chunked reduced-camera assembly, pass 1: one wave per chunk of <= kChunk triples of one
 // block; each lane accumulates A₁ᵀ(Z₁Z₂ᵀ)A₂ (36) and, for self-triples of a diagonal block,
 // A_eᵀ q_e (6); the wave reduces through LDS in fixed lane order (deterministic).
 __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
+    TRIAL_GUARD
     __shared__ double red[64][43];
     const int ch = blockIdx.x, lane = threadIdx.x;
     const int b = d.ch_blk[ch];
@@ -549,6 +409,7 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
 // pass 2: per block entry, sum its chunks in order, add Hpp + λI (diagonal), write the band /
 // dense matrix and b_s = b_p - Σ A_eᵀ q_e.
 __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
+    TRIAL_GUARD
     const int gid = blockIdx.x * kBlock + threadIdx.x;
     const int b = gid / 42, e = gid % 42;
     if (b >= d.nblk) return;
@@ -578,6 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
 // Semantics of Eigen::SimplicialLDLT as used by LinearSolverEigen: fails iff a pivot is 0.
 constexpr int kFacThreads = 1024;
 __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
+    TRIAL_GUARD
     __shared__ double T[kTile][kTile + 1];
     __shared__ double Dk[kTile];
     __shared__ int s_fail;
@@ -762,6 +624,7 @@ __device__ __forceinline__ double gj_inverse6(double M, int lane, bool &fail) {
 // hoisted; window slots advance incrementally (no runtime modulo in the loop).
 template <int BW>
 __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
+    TRIAL_GUARD
     constexpr int NT = kBandNT, W = BW + 1, NW = NT - 64;
     constexpr int NPAIR = BW * (BW + 1) / 2;             // trailing (wi >= wj >= 1) block pairs
     constexpr int PPT0 = (NPAIR * 36 - 36 + NW - 1) / NW; // pair entries per worker (pair 0 = wave 0)
@@ -1037,6 +900,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
 
 // ---------------------------------------------------------------- update + trial evaluation
 __global__ __launch_bounds__(kBlock) void k_pose_update(Dev d) {
+    TRIAL_GUARD
     __shared__ double sh[kBlock / 64];
     const int k = blockIdx.x * kBlock + threadIdx.x;
     double sc = 0.0;
@@ -1062,119 +926,10 @@ __global__ __launch_bounds__(kBlock) void k_pose_update(Dev d) {
     if (threadIdx.x == 0) d.part_ps[blockIdx.x] = s;
 }
 
-template <int DIM>
-__device__ __forceinline__ void landmark_update(const Dev &d, int l, double lam, int solve_ok, double &chi,
-                                                double &sc) {
-    const double *Xc = d.X_cur + (size_t)l * 4;
-    double *Xt = d.X_trial + (size_t)l * 4;
-    double x[4] = {0, 0, 0, 0};
-    if (solve_ok) {
-        double r[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = d.bl[(size_t)l * 4 + i];
-        for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
-            const int h = d.e_hidx[e];
-            if (h < 0) continue;
-            const double *A = d.A + (size_t)e * 12;
-            const double *B = d.B + (size_t)e * 8;
-            double ax0 = 0, ax1 = 0;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const double xk = d.xp[6 * h + k];
-                ax0 += A[k] * xk;
-                ax1 += A[6 + k] * xk;
-            }
-#pragma unroll
-            for (int i = 0; i < DIM; ++i) r[i] -= B[i] * ax0 + B[4 + i] * ax1;
-        }
-        double L[10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) L[k] = d.Lc[(size_t)l * 10 + k];
-        double y[4];
-#pragma unroll
-        for (int i = 0; i < DIM; ++i) {
-            double t = r[i];
-#pragma unroll
-            for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * y[p];
-            y[i] = t / L[pk(i, i)];
-        }
-#pragma unroll
-        for (int i = DIM - 1; i >= 0; --i) {
-            double t = y[i];
-#pragma unroll
-            for (int p = i + 1; p < DIM; ++p) t -= L[pk(p, i)] * x[p];
-            x[i] = t / L[pk(i, i)];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) d.xl[(size_t)l * 4 + i] = x[i];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = d.xl[(size_t)l * 4 + i];
-    }
-#pragma unroll
-    for (int i = 0; i < DIM; ++i) sc += x[i] * (lam * x[i] + d.bl[(size_t)l * 4 + i]);
-    double X[4];
-    if (DIM == 3) {
-        X[0] = Xc[0] + x[0];
-        X[1] = Xc[1] + x[1];
-        X[2] = Xc[2] + x[2];
-        X[3] = 0.0;
-    } else {
-        double in[4] = {Xc[0], Xc[1], Xc[2], Xc[3]};
-        orth_oplus(in, x, X);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Xt[i] = X[i];
-    double Lp[6];
-    if (DIM == 4) orth_to_pluker(X, Lp);
-    for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
-        if (!d.e_active[e]) continue;
-        const double *T = d.T_trial + (size_t)d.e_kf[e] * 12;
-        const double *obs = d.e_obs + (size_t)e * 4;
-        double err[2];
-        double delta;
-        if (DIM == 3) {
-            double z;
-            point_error(T, X, obs, d.cam, err, z);
-            delta = d.huber_pt;
-        } else {
-            line_error(T, Lp, obs, d.cam, err);
-            delta = d.huber_ln;
-        }
-        const double info = d.e_info[e];
-        const double c2 = err[0] * (info * err[0]) + err[1] * (info * err[1]);
-        d.chi2_last[e] = c2;
-        double rho0 = c2, rho1;
-        if (d.robust) huber(c2, delta, rho0, rho1);
-        chi += rho0;
-    }
-}
-__global__ __launch_bounds__(kBlock) void k_landmark_update(Dev d) {
-    __shared__ double sh[kBlock / 64];
-    const int l = blockIdx.x * kBlock + threadIdx.x;
-    double chi = 0.0, sc = 0.0;
-    if (l < d.n_lm) {
-        if (d.lm_active[l]) {
-            const double lam = d.ctrl->lambda;
-            const int ok = d.ctrl->solve_ok;
-            if (is_point_lm(d, l)) landmark_update<3>(d, l, lam, ok, chi, sc);
-            else landmark_update<4>(d, l, lam, ok, chi, sc);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) d.X_trial[(size_t)l * 4 + i] = d.X_cur[(size_t)l * 4 + i];
-        }
-    }
-    double s1 = block_sum<kBlock>(chi, sh);
-    double s2 = block_sum<kBlock>(sc, sh);
-    if (threadIdx.x == 0) {
-        d.part_lm[blockIdx.x] = s1;
-        d.part_lms[blockIdx.x] = s2;
-    }
-}
-
 // ---------------------------------------------------------------- edge-parallel trial path
 // per landmark: (Hll + λI) = L Lᵀ, g = L⁻¹ b_l
 __global__ __launch_bounds__(kBlock) void k_lm_chol(Dev d) {
+    TRIAL_GUARD
     const int l = blockIdx.x * kBlock + threadIdx.x;
     if (l >= d.n_lm) return;
     const double lam = d.ctrl->lambda;
@@ -1217,6 +972,7 @@ __global__ __launch_bounds__(kBlock) void k_lm_chol(Dev d) {
 }
 // per edge: Z_e = B_e L⁻ᵀ (rows solved with L), q_e = Z_e g
 __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
+    TRIAL_GUARD
     const int e = blockIdx.x * kBlock + threadIdx.x;
     if (e >= d.E) return;
     const int l = d.e_lm[e];
@@ -1254,6 +1010,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
 }
 // per edge: u_e = B_eᵀ (A_e x_p)
 __global__ __launch_bounds__(kBlock) void k_edge_backsub(Dev d) {
+    TRIAL_GUARD
     const int e = blockIdx.x * kBlock + threadIdx.x;
     if (e >= d.E || !d.ctrl->solve_ok) return;
     const int h = d.e_hidx[e];
@@ -1276,6 +1033,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_backsub(Dev d) {
 }
 // per landmark: x_l = L⁻ᵀ L⁻¹ (b_l - Σ u_e), oplus into the trial state, scale partial
 __global__ __launch_bounds__(kBlock) void k_lm_solve(Dev d) {
+    TRIAL_GUARD
     __shared__ double sh[kBlock / 64];
     const int l = blockIdx.x * kBlock + threadIdx.x;
     double sc = 0.0;
@@ -1346,6 +1104,7 @@ __global__ __launch_bounds__(kBlock) void k_lm_solve(Dev d) {
 }
 // per edge: χ² at the trial state (last-evaluated semantics), robust partial sums
 __global__ __launch_bounds__(kBlock) void k_edge_eval(Dev d) {
+    TRIAL_GUARD
     __shared__ double sh[kBlock / 64];
     const int e = blockIdx.x * kBlock + threadIdx.x;
     double chi = 0.0;
@@ -1366,15 +1125,16 @@ __global__ __launch_bounds__(kBlock) void k_edge_eval(Dev d) {
         const double c2 = err[0] * (info * err[0]) + err[1] * (info * err[1]);
         d.chi2_last[e] = c2;
         double rho0 = c2, rho1;
-        if (d.robust) huber(c2, delta, rho0, rho1);
+        if (d.ctrl->robust) huber(c2, delta, rho0, rho1);
         chi = rho0;
     }
     const double s1 = block_sum<kBlock>(chi, sh);
     if (threadIdx.x == 0) d.part_lm[blockIdx.x] = s1;
 }
 
-// OptimizationAlgorithmLevenberg trial decision
-__global__ __launch_bounds__(kBlock) void k_decide(Dev d, int max_trials) {
+// OptimizationAlgorithmLevenberg trial decision + optimize() loop control.
+__global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
+    TRIAL_GUARD
     __shared__ double sh[kBlock / 64];
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
@@ -1382,36 +1142,53 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d, int max_trials) {
     for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];
     const double tempChi0 = block_sum<kBlock>(a, sh);
     const double scale0 = block_sum<kBlock>(b, sh);
-    if (threadIdx.x == 0) {
-        Ctrl *c = d.ctrl;
-        double tempChi = tempChi0;
-        if (!c->solve_ok) tempChi = 1.7976931348623157e308;
-        const double scale = scale0 + 1e-3;
-        const double rho = (c->currentChi - tempChi) / scale;
-        c->tempChi = tempChi;
-        c->scale = scale;
-        c->rho = rho;
-        if (rho > 0 && isfinite(tempChi)) {
-            double alpha = 1. - pow((2 * rho - 1), 3);
-            alpha = fmin(alpha, 2. / 3.);
-            const double sf = fmax(1. / 3., alpha);
-            c->lambda *= sf;
-            c->ni = 2;
-            c->currentChi = tempChi;
-            c->accept = 1;
-            c->qmax += 1;
-        } else {
-            c->lambda *= c->ni;
-            c->ni *= 2;
-            c->accept = 0;
-            if (!isfinite(c->lambda)) c->broke = 1;
-            else c->qmax += 1;
-        }
+    if (threadIdx.x != 0) return;
+    Ctrl *c = d.ctrl;
+    c->steps += 1;
+    double tempChi = tempChi0;
+    if (!c->solve_ok) tempChi = 1.7976931348623157e308;
+    const double scale = scale0 + 1e-3;
+    const double rho = (c->currentChi - tempChi) / scale;
+    c->tempChi = tempChi;
+    c->scale = scale;
+    c->rho = rho;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        const double sf = fmax(1. / 3., alpha);
+        c->lambda *= sf;
+        c->ni = 2;
+        c->currentChi = tempChi;
+        c->accept = 1;
+        c->qmax += 1;
+    } else {
+        c->lambda *= c->ni;
+        c->ni *= 2;
+        c->accept = 0;
+        if (!isfinite(c->lambda)) c->broke = 1;
+        else c->qmax += 1;
+    }
+    c->commit_pending = c->accept;
+    const bool again = !c->broke && rho < 0 && c->qmax < c->max_trials;
+    if (again) return;  // another damped trial of this iteration
+    // end of OptimizationAlgorithmLevenberg::solve(iter)
+    const int terminate = (c->qmax == c->max_trials || rho == 0 || !isfinite(c->lambda)) ? 1 : 0;
+    if (c->ntrace < kTraceCap)
+        d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, c->qmax, terminate, c->chi2_start, c->currentChi,
+                                               c->lambda_start, c->lambda};
+    c->iters_done[c->stage] += 1;
+    c->iter += 1;
+    if (terminate || c->iter >= c->max_iters[c->stage]) {  // optimize() returns
+        c->chi2_final[c->stage] = c->currentChi;
+        if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
+        else c->all_done = 1;
+    } else {
+        c->need_iter = 1;
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_commit(Dev d) {
-    if (!d.ctrl->accept) return;
+    if (!d.ctrl->commit_pending) return;
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i < d.n_kf && d.kf_hidx[i] >= 0 && d.kf_active[i]) {
 #pragma unroll
@@ -1423,9 +1200,11 @@ __global__ __launch_bounds__(kBlock) void k_commit(Dev d) {
     }
 }
 
-// ---------------------------------------------------------------- outlier pass helpers
-// classification after stage 1 (src/mapHandler.cpp:6125-6147): level |= bad
-__global__ void k_classify(Dev d, double thr) {
+// ---------------------------------------------------------------- stage switch (initializeOptimization)
+// classification before a stage (src/mapHandler.cpp:6125-6147): level |= (χ² > thr || depth <= 0)
+__global__ void k_switch_classify(Dev d, double thr) {
+    const Ctrl *c = d.ctrl;
+    if (!c->switch_pending || !c->stage_classify[c->stage + 1]) return;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= d.E) return;
     bool bad = d.chi2_last[e] > thr;
@@ -1436,6 +1215,51 @@ __global__ void k_classify(Dev d, double thr) {
     }
     if (bad) d.e_level[e] = 1;
 }
+__global__ void k_switch_clear(Dev d) {
+    const Ctrl *c = d.ctrl;
+    if (!c->switch_pending) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d.n_lm) d.lm_active[i] = 0;
+    if (i < d.n_kf) d.kf_active[i] = 0;
+    if (i == 0) d.ctrl->any_active = 0;
+}
+// an edge is active iff its level is the optimised level (landmarks are never fixed); a vertex
+// iff it has an active edge (SparseOptimizer::initializeOptimization)
+__global__ void k_switch_activate(Dev d) {
+    Ctrl *c = d.ctrl;
+    if (!c->switch_pending) return;
+    const int lvl = c->stage_level[c->stage + 1];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    bool act = false;
+    if (e < d.E) {
+        act = d.e_level[e] == lvl;
+        d.e_active[e] = act ? 1 : 0;
+        if (act) {
+            d.lm_active[d.e_lm[e]] = 1;
+            d.kf_active[d.e_kf[e]] = 1;
+        }
+    }
+    if (__ballot(act) && (threadIdx.x & 63) == 0) atomicOr(&c->any_active, 1);
+}
+__global__ void k_switch_finish(Dev d) {
+    Ctrl *c = d.ctrl;
+    if (!c->switch_pending || threadIdx.x != 0) return;
+    c->switch_pending = 0;
+    c->stage += 1;
+    c->iter = 0;
+    c->robust = c->stage_robust[c->stage];
+    c->level = c->stage_level[c->stage];
+    if (!c->any_active) {  // _ivMap empty: optimize() returns -1 without iterating
+        c->iters_done[c->stage] = -1;
+        c->chi2_final[c->stage] = 0.0;
+        if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
+        else c->all_done = 1;
+    } else {
+        c->need_iter = 1;
+    }
+}
+
+// ---------------------------------------------------------------- outlier pass helpers
 // computeError() at the current state for edges of `level`
 __global__ void k_refresh(Dev d, int level) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
