@@ -18,6 +18,7 @@
 #include <map>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -30,6 +31,7 @@ namespace plba {
     do {                                                                                       \
         hipError_t _e = (expr);                                                                \
         if (_e != hipSuccess) {                                                                \
+            (void)hipGetLastError(); /* do not leak into the next launch check */              \
             ctx->set_error("HIP error %s at %s:%d: %s", hipGetErrorString(_e), __FILE__,       \
                            __LINE__, #expr);                                                   \
             return PLBA_E_DEVICE;                                                              \
@@ -111,6 +113,12 @@ struct plba_ctx {
             return PLBA_E_NOMEM;
         }
         allocs.push_back(p);
+        if constexpr (std::is_same<T, double>::value) {
+            // PLBA_POISON=1 (diagnostics only): fill f64 buffers with NaN to expose reads of
+            // memory no kernel wrote (a reused allocation is not zero).
+            const char *poison = getenv("PLBA_POISON");
+            if (poison && poison[0] == '1') (void)hipMemset(p, 0xFF, count * sizeof(T));
+        }
         return PLBA_OK;
     }
     hipEvent_t next_event() {
@@ -164,6 +172,7 @@ int timed(plba_ctx *ctx, int kid, F &&launch) {
         b = ctx->next_event();
         (void)hipEventRecord(a, ctx->stream);
     }
+    (void)hipGetLastError();  // launch errors below belong to this launch only
     launch();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -321,7 +330,9 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     for (auto &bk : blocks) first_blk[bk.second] = std::min(first_blk[bk.second], bk.first);
     int bw = 0;
     for (int h = 0; h < nf; ++h) bw = std::max(bw, h - first_blk[h]);
-    const bool band_mode = bw <= kBandMax;
+    // PLBA_FORCE_DENSE=1 (diagnostics only) routes a narrow envelope through the dense path.
+    const char *force_dense = getenv("PLBA_FORCE_DENSE");
+    const bool band_mode = bw <= kBandMax && !(force_dense && force_dense[0] == '1');
     if (band_mode) {  // every envelope block is written each trial (zeros where no landmark couples)
         for (int i2 = 0; i2 < nf; ++i2)
             for (int i1 = first_blk[i2]; i1 < i2; ++i1) {
@@ -483,9 +494,13 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 #undef UPLOAD
     if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)band_lds_bytes(bw, nf)));
-    PLBA_CHECK(hipMemset(d.e_level, 0, E));
+    // (zero-sized arrays are allocated with one element: clear exactly what alloc() gave)
+    // band blocks outside the envelope (w > i - first_blk[i]) are never assembled and must
+    // read as zero: the band kernel sweeps all BW block columns of every row
+    if (band_mode) PLBA_CHECK(hipMemset(d.Bd, 0, sizeof(double) * (size_t)nf * (bw + 1) * 36));
+    PLBA_CHECK(hipMemset(d.e_level, 0, std::max(E, 1)));
     PLBA_CHECK(hipMemset(d.xp, 0, sizeof(double) * std::max(n, 1)));
-    PLBA_CHECK(hipMemset(d.xl, 0, sizeof(double) * std::max(n_lm, 1) * 4));
+    PLBA_CHECK(hipMemset(d.xl, 0, sizeof(double) * std::max((size_t)n_lm * 4, (size_t)1)));
     PLBA_CHECK(hipMemset(d.chi2_last, 0, sizeof(double) * std::max(E, 1)));
     PLBA_CHECK(hipMemset(d.ctrl, 0, sizeof(Ctrl)));
     PLBA_CHECK(hipDeviceSynchronize());
@@ -702,7 +717,7 @@ int plba_reset_estimates(plba_ctx *ctx) {
     PLBA_CHECK(hipMemcpyAsync(d.X_cur, d.X_init, sizeof(double) * (size_t)d.n_lm * 4, hipMemcpyDeviceToDevice, ctx->stream));
     PLBA_CHECK(hipMemsetAsync(d.e_level, 0, std::max(d.E, 1), ctx->stream));
     PLBA_CHECK(hipMemsetAsync(d.xp, 0, sizeof(double) * std::max(d.n, 1), ctx->stream));
-    PLBA_CHECK(hipMemsetAsync(d.xl, 0, sizeof(double) * std::max(d.n_lm, 1) * 4, ctx->stream));
+    PLBA_CHECK(hipMemsetAsync(d.xl, 0, sizeof(double) * std::max((size_t)d.n_lm * 4, (size_t)1), ctx->stream));
     PLBA_CHECK(hipMemsetAsync(d.chi2_last, 0, sizeof(double) * std::max(d.E, 1), ctx->stream));
     std::fill(ctx->h_level.begin(), ctx->h_level.end(), 0);
     ctx->robust = 1;

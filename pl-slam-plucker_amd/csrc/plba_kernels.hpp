@@ -170,9 +170,11 @@ __device__ __forceinline__ void lds_barrier() {
         const Ctrl *cg = d.ctrl;                     \
         if (cg->all_done || !cg->need_iter) return;  \
     }
-#define TRIAL_GUARD                \
-    {                              \
-        if (d.ctrl->all_done) return; \
+// a stage skipped by k_switch_finish (no active edge) leaves switch_pending set: no trial
+#define TRIAL_GUARD                                          \
+    {                                                        \
+        const Ctrl *cg = d.ctrl;                             \
+        if (cg->all_done || cg->switch_pending) return;      \
     }
 
 __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {

@@ -152,9 +152,9 @@ def _project(Rcw, tcw, P, cam):
     return u, v, z
 
 
-def _tracks(rng, n_kf, count):
-    Lmax = min(8, n_kf)
-    Lmin = min(2, n_kf)
+def _tracks(rng, n_kf, count, lmin=2, lmax=8):
+    Lmax = min(lmax, n_kf)
+    Lmin = min(lmin, n_kf)
     L = rng.integers(Lmin, Lmax + 1, size=count)
     s = (rng.random(count) * (n_kf - L + 1)).astype(np.int64)
     return L, s
@@ -164,7 +164,7 @@ def _visible(Rcw, tcw, P, s, L, cam, margin):
     """P (M,3); tracks (s,L) -> bool (M,), all track KFs see P in the image."""
     M = P.shape[0]
     ok = np.ones(M, dtype=bool)
-    for j in range(8):
+    for j in range(int(L.max()) if M else 0):
         m = j < L
         if not m.any():
             break
@@ -187,7 +187,8 @@ def _sample_anchor(rng, Rwc, pwc, s, L, cam, depth_lo=2.0, depth_hi=8.0, margin=
 
 def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int] = None,
              n_ln: Optional[int] = None, seed: Optional[int] = None, fixed_frac: float = 0.1,
-             noise_px: float = 1.0, outlier_frac: float = 0.02, perturb: bool = True) -> Graph:
+             noise_px: float = 1.0, outlier_frac: float = 0.02, perturb: bool = True,
+             track_min: int = 2, track_max: int = 8) -> Graph:
     """Generate one window. ``name`` picks a config; keyword args override it."""
     base = CONFIGS.get(name, (10, 500, 0, 1000))
     n_kf = base[0] if n_kf is None else n_kf
@@ -207,7 +208,7 @@ def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int
     have = 0
     while have < n_pt:
         M = max(1024, 2 * (n_pt - have))
-        L, s = _tracks(rng, n_kf, M)
+        L, s = _tracks(rng, n_kf, M, track_min, track_max)
         P = _sample_anchor(rng, Rwc, pwc, s, L, cam)
         ok = _visible(Rcw, tcw, P, s, L, cam, margin=5.0)
         take = np.nonzero(ok)[0][: n_pt - have]
@@ -222,7 +223,7 @@ def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int
     have = 0
     while have < n_ln:
         M = max(1024, 2 * (n_ln - have))
-        L, s = _tracks(rng, n_kf, M)
+        L, s = _tracks(rng, n_kf, M, track_min, track_max)
         C = _sample_anchor(rng, Rwc, pwc, s, L, cam, margin=80.0)
         dvec = rng.normal(size=(M, 3))
         dvec /= np.linalg.norm(dvec, axis=1, keepdims=True)
@@ -231,7 +232,7 @@ def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int
         P2 = C + 0.5 * length[:, None] * dvec
         ok = _visible(Rcw, tcw, P1, s, L, cam, 5.0) & _visible(Rcw, tcw, P2, s, L, cam, 5.0)
         # projected segment length >= 15 px in every track KF (well-defined image line)
-        for j in range(8):
+        for j in range(int(L.max())):
             m = j < L
             kf = np.where(m, s + j, s)
             u1, v1, _ = _project(Rcw[kf], tcw[kf], P1, cam)
