@@ -1,0 +1,99 @@
+/*
+ * plslam_host.h — C ABI of the host-side mirror of the reference's map objects and of
+ *   void PLSLAM::MapHandler::localBundleAdjustmentForPlukerWithG2O()
+ *   (reference: include/mapHandler.h:134, src/mapHandler.cpp:5851-6323)
+ *
+ * The C++ classes behind it (pl-slam-plucker_amd/host/plslam_map.hpp) restate the state the
+ * reference LBA reads and mutates — KeyFrame (include/keyFrame.h:50-71), MapPoint / MapLine
+ * (include/mapFeatures.h:39-107), MapHandler::{map_keyframes, map_points, map_lines,
+ * map_points_kf_idx, full_graph} (include/mapHandler.h:141-151) — and run the reference's
+ * host logic around the solve: window gather (A1, src/mapHandler.cpp:5868-5921), graph
+ * marshalling (A1b, :5923-6117), post-solve outlier bookkeeping (A1d, :6154-6293) and
+ * write-back (A1e, :6296-6319). The solve itself (A1c) goes through plba.h on the GPU.
+ *
+ * These entry points exist for bindings and tests; a C++ caller (the reference's own
+ * MapHandler) uses the classes directly — see INTEGRATION.md.
+ *
+ * Status codes are plba.h's (PLBA_OK / PLBA_E_*); nothing throws or exits.
+ */
+#ifndef PLSLAM_HOST_H
+#define PLSLAM_HOST_H
+
+#include <stdint.h>
+
+#include "plba.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct plslam_map plslam_map;
+
+/* Solver hook: solves one marshalled window (plba_graph) into plba_result.
+ * NULL (the default) = the MI355X backend of plba.h (one plba context per map, reused across
+ * LBA calls). Tests install a stub here to drive the host bookkeeping without a GPU. */
+typedef int (*plslam_solve_fn)(void *user, const plba_graph *g, plba_result *r);
+
+/* Statistics of one LBA call (the counters the reference prints, src/mapHandler.cpp:6147,6216,6290). */
+typedef struct plslam_lba_stats {
+    int32_t n_free_kf, n_fixed_kf;         /* idx_nofix_kfs / idx_fix_kfs sizes                      */
+    int32_t n_pt, n_ln, n_ept, n_eln;      /* local landmarks and edges in the window                */
+    int32_t bad_line_stage1;               /* "Bad Obs" after optimize(5) (:6147)                     */
+    int32_t bad_point_obs, actually_bad_point_obs;   /* (:6216)                                     */
+    int32_t bad_line_obs, actually_bad_line_obs;     /* (:6290)                                     */
+    int32_t iters[2];
+    double  chi2[2];
+    double  gather_ms, solve_ms, bookkeeping_ms;
+} plslam_lba_stats;
+
+int         plslam_map_create(plslam_map **m, double fx, double fy, double cx, double cy, const plba_opts *opts);
+int         plslam_map_destroy(plslam_map *m);
+const char *plslam_map_last_error(plslam_map *m);
+int         plslam_set_solver(plslam_map *m, plslam_solve_fn fn, void *user);
+
+/* KeyFrame(sf, kf_idx) placed at map_keyframes[kf_idx]; T_kf_w is row-major 4x4 (camera->world).
+ * pt_idx / ls_idx are the idx fields of the KF's stereo_frame->stereo_pt / stereo_ls features. */
+int plslam_add_keyframe(plslam_map *m, int32_t kf_idx, const double T_kf_w[16], int32_t n_pt_feat,
+                        const int32_t *pt_idx, int32_t n_ls_feat, const int32_t *ls_idx);
+/* MapPoint(idx, point3D, desc, kf_obs, obs, dir, sigma2) at map_points[idx] (src/mapFeatures.cpp:38-50). */
+int plslam_add_point(plslam_map *m, int32_t idx, const double xyz[3], const uint8_t *desc, int32_t desc_bytes,
+                     int32_t kf, const double obs[2], const double dir[3], double sigma2);
+/* MapPoint::addMapPointObservation (src/mapFeatures.cpp:52-60). */
+int plslam_point_add_observation(plslam_map *m, int32_t idx, const uint8_t *desc, int32_t kf, const double obs[2],
+                                 const double dir[3], double sigma2);
+/* Plücker MapLine(idx, NDw, desc, kf_obs, obs, sigma2) at map_lines[idx] (src/mapFeatures.cpp:114-122). */
+int plslam_add_line(plslam_map *m, int32_t idx, const double NDw[6], const uint8_t *desc, int32_t desc_bytes,
+                    int32_t kf, const double obs[4], double sigma2);
+/* MapLine::addMapLineObservation(desc, kf_obs, obs4, sigma2) (src/mapFeatures.cpp:132-138). */
+int plslam_line_add_observation(plslam_map *m, int32_t idx, const uint8_t *desc, int32_t kf, const double obs[4],
+                                double sigma2);
+/* the `local` flag of a keyframe (kind 0), point (1) or line (2). */
+int plslam_set_local(plslam_map *m, int32_t kind, int32_t idx, int32_t local);
+/* full_graph (n x n, row-major); map_points_kf_idx[kf] = lm[0..n) (creates the key, even empty) */
+int plslam_set_full_graph(plslam_map *m, int32_t n, const uint32_t *g);
+int plslam_get_full_graph(plslam_map *m, int32_t n, uint32_t *g);
+int plslam_kf_idx_set(plslam_map *m, int32_t kf, const int32_t *lm, int32_t n);
+int plslam_kf_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int32_t *n);
+
+/* MapHandler::localBundleAdjustmentForPlukerWithG2O() */
+int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats);
+
+/* State readers (any pointer may be NULL). n_obs receives the observation count; the list
+ * outputs are written up to `cap` entries. */
+int plslam_get_keyframe(plslam_map *m, int32_t kf_idx, double T_kf_w[16], int32_t *local, int32_t *pt_idx,
+                        int32_t pt_cap, int32_t *ls_idx, int32_t ls_cap);
+int plslam_get_point(plslam_map *m, int32_t idx, double xyz[3], int32_t *inlier, int32_t *local, int32_t *n_obs,
+                     int32_t *kf_obs, double *obs, double *dir, double *sigma, int32_t cap, uint8_t *med_desc,
+                     double med_dir[3]);
+int plslam_get_line(plslam_map *m, int32_t idx, double NDw[6], int32_t *inlier, int32_t *local, int32_t *n_obs,
+                    int32_t *kf_obs, double *obs, double *sigma, int32_t cap, uint8_t *med_desc);
+
+/* MapLine::changePlukerToOrth / changeOrthToPluker (src/mapFeatures.cpp:186-221) */
+void plslam_pluker_to_orth(const double NDw[6], double orth[4]);
+void plslam_orth_to_pluker(const double orth[4], double NDw[6]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLSLAM_HOST_H */

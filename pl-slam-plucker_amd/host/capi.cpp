@@ -1,0 +1,237 @@
+// C ABI of the host mirror (include/plslam_host.h) over plslam::MapHandler.
+#include "plslam_host.h"
+
+#include <cstring>
+#include <new>
+
+#include "plslam_map.hpp"
+
+using namespace plslam;
+
+struct plslam_map {
+    MapHandler mh;
+    int desc_bytes = 32;
+    plslam_map(double fx, double fy, double cx, double cy, const plba_opts *o) : mh(fx, fy, cx, cy, o) {}
+};
+
+namespace {
+Desc make_desc(const uint8_t *d, int n) { return d ? Desc(d, d + n) : Desc((size_t)n, 0); }
+
+template <typename T>
+bool slot_ok(std::vector<T *> &v, int idx) {
+    return idx >= 0 && idx < (int)v.size() && v[idx] != nullptr;
+}
+template <typename T>
+void place(std::vector<T *> &v, int idx, T *p) {
+    if ((int)v.size() <= idx) v.resize(idx + 1, nullptr);
+    delete v[idx];
+    v[idx] = p;
+}
+}  // namespace
+
+extern "C" {
+
+int plslam_map_create(plslam_map **m, double fx, double fy, double cx, double cy, const plba_opts *opts) {
+    if (!m) return PLBA_E_INVALID;
+    *m = new (std::nothrow) plslam_map(fx, fy, cx, cy, opts);
+    return *m ? PLBA_OK : PLBA_E_NOMEM;
+}
+
+int plslam_map_destroy(plslam_map *m) {
+    delete m;
+    return PLBA_OK;
+}
+
+const char *plslam_map_last_error(plslam_map *m) { return m ? m->mh.lastError().c_str() : "null map"; }
+
+int plslam_set_solver(plslam_map *m, plslam_solve_fn fn, void *user) {
+    if (!m) return PLBA_E_INVALID;
+    m->mh.setSolver(fn, user);
+    return PLBA_OK;
+}
+
+int plslam_add_keyframe(plslam_map *m, int32_t kf_idx, const double T_kf_w[16], int32_t n_pt_feat,
+                        const int32_t *pt_idx, int32_t n_ls_feat, const int32_t *ls_idx) {
+    if (!m || kf_idx < 0 || !T_kf_w || n_pt_feat < 0 || n_ls_feat < 0) return PLBA_E_INVALID;
+    auto *k = new KeyFrame();
+    k->kf_idx = kf_idx;
+    std::memcpy(k->T_kf_w.data(), T_kf_w, sizeof(double) * 16);
+    if (pt_idx) k->stereo_frame.stereo_pt_idx.assign(pt_idx, pt_idx + n_pt_feat);
+    if (ls_idx) k->stereo_frame.stereo_ls_idx.assign(ls_idx, ls_idx + n_ls_feat);
+    place(m->mh.map_keyframes, kf_idx, k);
+    return PLBA_OK;
+}
+
+int plslam_add_point(plslam_map *m, int32_t idx, const double xyz[3], const uint8_t *desc, int32_t desc_bytes,
+                     int32_t kf, const double obs[2], const double dir[3], double sigma2) {
+    if (!m || idx < 0 || !xyz || !obs || desc_bytes <= 0) return PLBA_E_INVALID;
+    m->desc_bytes = desc_bytes;
+    Vec3 d = dir ? Vec3{dir[0], dir[1], dir[2]} : Vec3{0, 0, 0};
+    place(m->mh.map_points, idx,
+          new MapPoint(idx, Vec3{xyz[0], xyz[1], xyz[2]}, make_desc(desc, desc_bytes), kf, Vec2{obs[0], obs[1]}, d,
+                       sigma2));
+    return PLBA_OK;
+}
+
+int plslam_point_add_observation(plslam_map *m, int32_t idx, const uint8_t *desc, int32_t kf, const double obs[2],
+                                 const double dir[3], double sigma2) {
+    if (!m || !obs || !slot_ok(m->mh.map_points, idx)) return PLBA_E_INVALID;
+    Vec3 d = dir ? Vec3{dir[0], dir[1], dir[2]} : Vec3{0, 0, 0};
+    m->mh.map_points[idx]->addMapPointObservation(make_desc(desc, m->desc_bytes), kf, Vec2{obs[0], obs[1]}, d, sigma2);
+    return PLBA_OK;
+}
+
+int plslam_add_line(plslam_map *m, int32_t idx, const double NDw[6], const uint8_t *desc, int32_t desc_bytes,
+                    int32_t kf, const double obs[4], double sigma2) {
+    if (!m || idx < 0 || !NDw || !obs || desc_bytes <= 0) return PLBA_E_INVALID;
+    m->desc_bytes = desc_bytes;
+    Vec6 L;
+    std::memcpy(L.data(), NDw, sizeof(double) * 6);
+    place(m->mh.map_lines, idx,
+          new MapLine(idx, L, make_desc(desc, desc_bytes), kf, Vec4{obs[0], obs[1], obs[2], obs[3]}, sigma2));
+    return PLBA_OK;
+}
+
+int plslam_line_add_observation(plslam_map *m, int32_t idx, const uint8_t *desc, int32_t kf, const double obs[4],
+                                double sigma2) {
+    if (!m || !obs || !slot_ok(m->mh.map_lines, idx)) return PLBA_E_INVALID;
+    m->mh.map_lines[idx]->addMapLineObservation(make_desc(desc, m->desc_bytes), kf,
+                                                Vec4{obs[0], obs[1], obs[2], obs[3]}, sigma2);
+    return PLBA_OK;
+}
+
+int plslam_set_local(plslam_map *m, int32_t kind, int32_t idx, int32_t local) {
+    if (!m) return PLBA_E_INVALID;
+    switch (kind) {
+        case 0:
+            if (!slot_ok(m->mh.map_keyframes, idx)) return PLBA_E_INVALID;
+            m->mh.map_keyframes[idx]->local = local != 0;
+            return PLBA_OK;
+        case 1:
+            if (!slot_ok(m->mh.map_points, idx)) return PLBA_E_INVALID;
+            m->mh.map_points[idx]->local = local != 0;
+            return PLBA_OK;
+        case 2:
+            if (!slot_ok(m->mh.map_lines, idx)) return PLBA_E_INVALID;
+            m->mh.map_lines[idx]->local = local != 0;
+            return PLBA_OK;
+        default:
+            return PLBA_E_INVALID;
+    }
+}
+
+int plslam_set_full_graph(plslam_map *m, int32_t n, const uint32_t *g) {
+    if (!m || n < 0 || (n && !g)) return PLBA_E_INVALID;
+    m->mh.full_graph.assign(n, std::vector<unsigned int>(n, 0));
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) m->mh.full_graph[i][j] = g[(size_t)i * n + j];
+    return PLBA_OK;
+}
+
+int plslam_get_full_graph(plslam_map *m, int32_t n, uint32_t *g) {
+    if (!m || !g || n != (int)m->mh.full_graph.size()) return PLBA_E_INVALID;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) g[(size_t)i * n + j] = m->mh.full_graph[i][j];
+    return PLBA_OK;
+}
+
+int plslam_kf_idx_set(plslam_map *m, int32_t kf, const int32_t *lm, int32_t n) {
+    if (!m || n < 0 || (n && !lm)) return PLBA_E_INVALID;
+    m->mh.map_points_kf_idx[kf].assign(lm, lm + n);
+    return PLBA_OK;
+}
+
+int plslam_kf_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int32_t *n) {
+    if (!m || !n) return PLBA_E_INVALID;
+    auto it = m->mh.map_points_kf_idx.find(kf);
+    if (it == m->mh.map_points_kf_idx.end()) {
+        *n = -1;
+        return PLBA_OK;
+    }
+    *n = (int32_t)it->second.size();
+    for (int i = 0; out && i < *n && i < cap; ++i) out[i] = it->second[i];
+    return PLBA_OK;
+}
+
+int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats) {
+    if (!m) return PLBA_E_INVALID;
+    LbaStats st;
+    const int rc = m->mh.localBundleAdjustmentForPlukerWithG2O(&st);
+    if (rc) return rc;
+    if (stats) {
+        stats->n_free_kf = st.n_free_kf; stats->n_fixed_kf = st.n_fixed_kf;
+        stats->n_pt = st.n_pt; stats->n_ln = st.n_ln; stats->n_ept = st.n_ept; stats->n_eln = st.n_eln;
+        stats->bad_line_stage1 = st.bad_line_stage1;
+        stats->bad_point_obs = st.bad_point_obs; stats->actually_bad_point_obs = st.actually_bad_point_obs;
+        stats->bad_line_obs = st.bad_line_obs; stats->actually_bad_line_obs = st.actually_bad_line_obs;
+        stats->iters[0] = st.iters[0]; stats->iters[1] = st.iters[1];
+        stats->chi2[0] = st.chi2[0]; stats->chi2[1] = st.chi2[1];
+        stats->gather_ms = st.gather_ms; stats->solve_ms = st.solve_ms; stats->bookkeeping_ms = st.bookkeeping_ms;
+    }
+    return PLBA_OK;
+}
+
+int plslam_get_keyframe(plslam_map *m, int32_t kf_idx, double T_kf_w[16], int32_t *local, int32_t *pt_idx,
+                        int32_t pt_cap, int32_t *ls_idx, int32_t ls_cap) {
+    if (!m || !slot_ok(m->mh.map_keyframes, kf_idx)) return PLBA_E_INVALID;
+    const KeyFrame *k = m->mh.map_keyframes[kf_idx];
+    if (T_kf_w) std::memcpy(T_kf_w, k->T_kf_w.data(), sizeof(double) * 16);
+    if (local) *local = k->local;
+    for (int i = 0; pt_idx && i < pt_cap && i < (int)k->stereo_frame.stereo_pt_idx.size(); ++i)
+        pt_idx[i] = k->stereo_frame.stereo_pt_idx[i];
+    for (int i = 0; ls_idx && i < ls_cap && i < (int)k->stereo_frame.stereo_ls_idx.size(); ++i)
+        ls_idx[i] = k->stereo_frame.stereo_ls_idx[i];
+    return PLBA_OK;
+}
+
+int plslam_get_point(plslam_map *m, int32_t idx, double xyz[3], int32_t *inlier, int32_t *local, int32_t *n_obs,
+                     int32_t *kf_obs, double *obs, double *dir, double *sigma, int32_t cap, uint8_t *med_desc,
+                     double med_dir[3]) {
+    if (!m || !slot_ok(m->mh.map_points, idx)) return PLBA_E_INVALID;
+    const MapPoint *p = m->mh.map_points[idx];
+    if (xyz) std::memcpy(xyz, p->point3D.data(), sizeof(double) * 3);
+    if (inlier) *inlier = p->inlier;
+    if (local) *local = p->local;
+    if (n_obs) *n_obs = (int32_t)p->kf_obs_list.size();
+    for (int i = 0; i < cap && i < (int)p->kf_obs_list.size(); ++i) {
+        if (kf_obs) kf_obs[i] = p->kf_obs_list[i];
+        if (obs) { obs[2 * i] = p->obs_list[i][0]; obs[2 * i + 1] = p->obs_list[i][1]; }
+        if (dir) for (int k = 0; k < 3; ++k) dir[3 * i + k] = p->dir_list[i][k];
+    }
+    for (int i = 0; sigma && i < cap && i < (int)p->sigma_list.size(); ++i) sigma[i] = p->sigma_list[i];
+    if (med_desc) std::memcpy(med_desc, p->med_desc.data(), p->med_desc.size());
+    if (med_dir) std::memcpy(med_dir, p->med_obs_dir.data(), sizeof(double) * 3);
+    return PLBA_OK;
+}
+
+int plslam_get_line(plslam_map *m, int32_t idx, double NDw[6], int32_t *inlier, int32_t *local, int32_t *n_obs,
+                    int32_t *kf_obs, double *obs, double *sigma, int32_t cap, uint8_t *med_desc) {
+    if (!m || !slot_ok(m->mh.map_lines, idx)) return PLBA_E_INVALID;
+    const MapLine *l = m->mh.map_lines[idx];
+    if (NDw) std::memcpy(NDw, l->NDw.data(), sizeof(double) * 6);
+    if (inlier) *inlier = l->inlier;
+    if (local) *local = l->local;
+    if (n_obs) *n_obs = (int32_t)l->kf_obs_list.size();
+    for (int i = 0; i < cap && i < (int)l->kf_obs_list.size(); ++i) {
+        if (kf_obs) kf_obs[i] = l->kf_obs_list[i];
+        if (obs) for (int k = 0; k < 4; ++k) obs[4 * i + k] = l->NDw_obs_list[i][k];
+    }
+    for (int i = 0; sigma && i < cap && i < (int)l->sigma_list.size(); ++i) sigma[i] = l->sigma_list[i];
+    if (med_desc) std::memcpy(med_desc, l->med_desc.data(), l->med_desc.size());
+    return PLBA_OK;
+}
+
+void plslam_pluker_to_orth(const double NDw[6], double orth[4]) {
+    Vec6 L;
+    std::memcpy(L.data(), NDw, sizeof(double) * 6);
+    const Vec4 o = MapLine::changePlukerToOrth(L);
+    std::memcpy(orth, o.data(), sizeof(double) * 4);
+}
+
+void plslam_orth_to_pluker(const double orth[4], double NDw[6]) {
+    const Vec4 o{orth[0], orth[1], orth[2], orth[3]};
+    const Vec6 L = MapLine::changeOrthToPluker(o);
+    std::memcpy(NDw, L.data(), sizeof(double) * 6);
+}
+
+}  // extern "C"

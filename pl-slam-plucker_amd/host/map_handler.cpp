@@ -1,0 +1,511 @@
+// MapHandler::localBundleAdjustmentForPlukerWithG2O host logic (src/mapHandler.cpp:5851-6323)
+// around the MI355X solve of plba.h. See plslam_map.hpp.
+#include "plslam_map.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+
+namespace plslam {
+
+// ----------------------------------------------------------------------------- helpers
+int hamming(const Desc &a, const Desc &b) {  // cv::norm(a, b, NORM_HAMMING)
+    const size_t n = std::min(a.size(), b.size());
+    int d = 0;
+    for (size_t i = 0; i < n; ++i) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+    return d;
+}
+
+// General 4x4 inverse by cofactors (what Matrix4d::inverse() computes for the pose matrices,
+// src/mapHandler.cpp:5940,5959,6302).
+Mat4 inverse4(const Mat4 &m) {
+    Mat4 inv;
+    inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] +
+             m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] -
+             m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] +
+             m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] -
+              m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] -
+             m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] +
+             m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] -
+             m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] +
+              m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] +
+             m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] -
+             m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] +
+              m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] -
+              m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] -
+             m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] +
+             m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] -
+              m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] +
+              m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+    const double r = 1.0 / det;
+    for (double &v : inv) v *= r;
+    return inv;
+}
+
+// ----------------------------------------------------------------------------- MapPoint
+MapPoint::MapPoint(int idx_, const Vec3 &p, const Desc &desc, int kf_obs, const Vec2 &obs, const Vec3 &dir,
+                   double sigma2)
+    : idx(idx_), inlier(true), point3D(p) {  // src/mapFeatures.cpp:38-50
+    desc_list.push_back(desc);
+    obs_list.push_back(obs);
+    kf_obs_list.push_back(kf_obs);
+    dir_list.push_back(dir);
+    sigma_list.push_back(sigma2);
+    med_obs_dir = dir;
+    med_desc = desc;
+}
+
+void MapPoint::addMapPointObservation(const Desc &desc, int kf_obs, const Vec2 &obs, const Vec3 &dir,
+                                      double sigma2) {  // src/mapFeatures.cpp:52-60
+    desc_list.push_back(desc);
+    obs_list.push_back(obs);
+    kf_obs_list.push_back(kf_obs);
+    dir_list.push_back(dir);
+    sigma_list.push_back(sigma2);
+    updateAverageDescDir();
+}
+
+// Index of the descriptor with the smallest median Hamming distance to the others
+// (src/mapFeatures.cpp:57-86). The reference reads dist_idx[int(1+0.5*(n-1))], one past the
+// end when n == 1; that single-observation case is clamped to the only descriptor here.
+static int median_descriptor(const std::vector<Desc> &desc_list) {
+    const int n = (int)desc_list.size();
+    std::vector<int> conf((size_t)n * n, 0);
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j) {
+            const int d = hamming(desc_list[i], desc_list[j]);
+            conf[(size_t)i * n + j] = d;
+            conf[(size_t)j * n + i] = d;
+        }
+    int max_dist = 99999, max_idx = 0;
+    std::vector<int> dist_idx(n);
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < n; ++j) dist_idx[j] = conf[(size_t)i * n + j];
+        std::sort(dist_idx.begin(), dist_idx.end());
+        const int k = std::min(int(1 + 0.5 * (n - 1)), n - 1);
+        const int idx_median = dist_idx[k];
+        if (idx_median < max_dist) {
+            max_dist = idx_median;
+            max_idx = i;
+        }
+    }
+    return max_idx;
+}
+
+void MapPoint::updateAverageDescDir() {
+    const int n = (int)desc_list.size();
+    if (n == 0) return;
+    med_desc = desc_list[median_descriptor(desc_list)];
+    // direction: mean of the observation directions (the reference sums into an
+    // uninitialised Vector3d, src/mapFeatures.cpp:89-92; zero-initialised here)
+    Vec3 s{0.0, 0.0, 0.0};
+    for (int i = 0; i < (int)dir_list.size() && i < n; ++i)
+        for (int k = 0; k < 3; ++k) s[k] += dir_list[i][k];
+    for (int k = 0; k < 3; ++k) med_obs_dir[k] = s[k] / n;
+}
+
+// ----------------------------------------------------------------------------- MapLine
+MapLine::MapLine(int idx_, const Vec6 &NDw_, const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2)
+    : idx(idx_), inlier(true), NDw(NDw_) {  // src/mapFeatures.cpp:114-122
+    desc_list.push_back(desc);
+    NDw_obs_list.push_back(obs);
+    kf_obs_list.push_back(kf_obs);
+    sigma_list.push_back(sigma2);
+    med_desc = desc;
+}
+
+void MapLine::addMapLineObservation(const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2) {
+    desc_list.push_back(desc);  // src/mapFeatures.cpp:132-138
+    NDw_obs_list.push_back(obs);
+    sigma_list.push_back(sigma2);
+    kf_obs_list.push_back(kf_obs);
+    updateAverageDescDir();
+}
+
+void MapLine::updateAverageDescDir() {  // src/mapFeatures.cpp:140-184 (USE_LINE_PLUKER)
+    if (desc_list.empty()) return;
+    med_desc = desc_list[median_descriptor(desc_list)];
+}
+
+static inline double norm3(const double *v) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+
+// changePlukerToOrth with getOrhtRFromPluker / getOrthWFromPluker (src/mapFeatures.cpp:186-249)
+Vec4 MapLine::changePlukerToOrth(const Vec6 &L) {
+    const double *n = L.data(), *d = L.data() + 3;
+    const double nn = norm3(n), dn = norm3(d);
+    double c[3] = {n[1] * d[2] - n[2] * d[1], n[2] * d[0] - n[0] * d[2], n[0] * d[1] - n[1] * d[0]};
+    const double cn = norm3(c);
+    const double u1[3] = {n[0] / nn, n[1] / nn, n[2] / nn};
+    const double u2[3] = {d[0] / dn, d[1] / dn, d[2] / dn};
+    const double u3[3] = {c[0] / cn, c[1] / cn, c[2] / cn};
+    const double f = std::sqrt(nn * nn + dn * dn);
+    Vec4 o;
+    o[0] = std::atan2(u2[2], u3[2]);
+    o[1] = std::asin(-u1[2]);
+    o[2] = std::atan2(u1[1], u1[0]);
+    o[3] = std::asin(dn / f);
+    return o;
+}
+
+// changeOrthToPluker (src/mapFeatures.cpp:203-221): [w1·R.col(0); w2·R.col(1)]
+Vec6 MapLine::changeOrthToPluker(const Vec4 &o) {
+    const double s1 = std::sin(o[0]), c1 = std::cos(o[0]);
+    const double s2 = std::sin(o[1]), c2 = std::cos(o[1]);
+    const double s3 = std::sin(o[2]), c3 = std::cos(o[2]);
+    const double w1 = std::cos(o[3]), w2 = std::sin(o[3]);
+    Vec6 L;
+    L[0] = w1 * (c2 * c3);
+    L[1] = w1 * (c2 * s3);
+    L[2] = w1 * (-s2);
+    L[3] = w2 * (s1 * s2 * c3 - c1 * s3);
+    L[4] = w2 * (s1 * s2 * s3 + c1 * c3);
+    L[5] = w2 * (s1 * c2);
+    return L;
+}
+
+// ----------------------------------------------------------------------------- Window
+plba_graph Window::graph(double fx, double fy, double cx, double cy) const {
+    plba_graph g{};
+    g.n_kf = (int32_t)kf_id.size();
+    g.n_pt = (int32_t)pt_id.size();
+    g.n_ln = (int32_t)ln_id.size();
+    g.n_ept = (int32_t)ept_lm.size();
+    g.n_eln = (int32_t)eln_lm.size();
+    g.fx = fx; g.fy = fy; g.cx = cx; g.cy = cy;
+    g.kf_Tcw = kf_Tcw.data(); g.kf_fixed = kf_fixed.data(); g.kf_id = kf_id.data();
+    g.pt_xyz = pt_xyz.data(); g.pt_id = pt_id.data();
+    g.ln_orth = ln_orth.data(); g.ln_id = ln_id.data();
+    g.ept_lm = ept_lm.data(); g.ept_kf = ept_kf.data(); g.ept_obs = ept_obs.data(); g.ept_info = ept_info.data();
+    g.eln_lm = eln_lm.data(); g.eln_kf = eln_kf.data(); g.eln_obs = eln_obs.data(); g.eln_info = eln_info.data();
+    // const float thHuberMono = sqrt(5.991)  (src/mapHandler.cpp:5978, 6035)
+    g.huber_pt = (double)(float)std::sqrt(5.991);
+    g.huber_ln = (double)(float)std::sqrt(5.991);
+    return g;
+}
+
+// ----------------------------------------------------------------------------- MapHandler
+MapHandler::MapHandler(double fx, double fy, double cx, double cy, const plba_opts *opts)
+    : fx_(fx), fy_(fy), cx_(cx), cy_(cy) {
+    if (opts) {
+        opts_ = *opts;
+        have_opts_ = true;
+    }
+}
+
+MapHandler::~MapHandler() {
+    if (ctx_) plba_destroy(ctx_);
+    for (auto *k : map_keyframes) delete k;
+    for (auto *p : map_points) delete p;
+    for (auto *l : map_lines) delete l;
+}
+
+void MapHandler::setError(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    err_ = buf;
+}
+
+// A1 + A1b: window gather (src/mapHandler.cpp:5868-5921) and graph marshalling (:5923-6117).
+int MapHandler::gatherWindow(Window &w) {
+    w = Window{};
+    // validate every observation first (the reference exit(0)s mid-gather, :5891-5895, 5907-5911)
+    auto valid_kf = [&](int o) {
+        return o >= 0 && o < (int)map_keyframes.size() && map_keyframes[o] && map_keyframes[o]->kf_idx == o;
+    };
+    for (auto *p : map_points)
+        if (p && p->local)
+            for (int o : p->kf_obs_list)
+                if (!valid_kf(o)) {
+                    setError("[Wrong index in the map_keyframes and MapPoint obs] point %d obs kf %d", p->idx, o);
+                    return PLBA_E_INVALID;
+                }
+    for (auto *l : map_lines)
+        if (l && l->local)
+            for (int o : l->kf_obs_list)
+                if (!valid_kf(o)) {
+                    setError("[Wrong index in the map_keyframes and MapLine obs] line %d obs kf %d", l->idx, o);
+                    return PLBA_E_INVALID;
+                }
+
+    std::map<int, KeyFrame *> idx_fix_kfs, idx_nofix_kfs, idx_all_kfs;
+    for (auto *k : map_keyframes)  // :5870-5875
+        if (k && k->local) {
+            idx_nofix_kfs.insert({k->kf_idx, k});
+            idx_all_kfs.insert({k->kf_idx, k});
+        }
+    for (auto *p : map_points)
+        if (p && p->local) w.local_pt.push_back(p);  // :5877-5881
+    for (auto *l : map_lines)
+        if (l && l->local) w.local_ls.push_back(l);  // :5882-5886
+    // observers outside the local set become fixed — and local, as a side effect (:5888-5919)
+    auto add_observers = [&](const std::vector<int> &obs) {
+        for (int o : obs) {
+            KeyFrame *k = map_keyframes[o];
+            if (!k->local) {
+                idx_fix_kfs.insert({o, k});
+                idx_all_kfs.insert({o, k});
+                k->local = true;
+            }
+        }
+    };
+    for (auto *p : w.local_pt) add_observers(p->kf_obs_list);
+    for (auto *l : w.local_ls) add_observers(l->kf_obs_list);
+
+    // pose vertices: free KFs (id 0 fixed), then the fixed observers (:5931-5967)
+    std::map<int, int> kf_pos;  // kf_idx -> position in the kf arrays
+    auto add_pose = [&](KeyFrame *k, bool fixed) {
+        const Mat4 Tcw = inverse4(k->T_kf_w);
+        kf_pos[k->kf_idx] = (int)w.kf_id.size();
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) w.kf_Tcw.push_back(Tcw[r * 4 + c]);
+        w.kf_fixed.push_back(fixed ? 1 : 0);
+        w.kf_id.push_back(k->kf_idx);
+        if (w.max_kf_id < k->kf_idx + 1) w.max_kf_id = k->kf_idx + 1;
+    };
+    for (auto &kv : idx_nofix_kfs) {
+        w.nofix_kfs.push_back(kv.second);
+        add_pose(kv.second, kv.first == 0);
+    }
+    for (auto &kv : idx_fix_kfs) {
+        w.fix_kfs.push_back(kv.second);
+        add_pose(kv.second, true);
+    }
+
+    // point vertices + edges (:5976-6027)
+    w.maxPointId = w.max_kf_id;
+    for (size_t li = 0; li < w.local_pt.size(); ++li) {
+        MapPoint *p = w.local_pt[li];
+        const int id = p->idx + w.max_kf_id + 1;
+        w.pt_id.push_back(id);
+        for (int k = 0; k < 3; ++k) w.pt_xyz.push_back(p->point3D[k]);
+        for (size_t i = 0; i < p->kf_obs_list.size(); ++i) {
+            const int kf_id = p->kf_obs_list[i];
+            w.ept_lm.push_back((int32_t)li);
+            w.ept_kf.push_back(kf_pos.at(kf_id));
+            w.ept_obs.push_back(p->obs_list[i][0]);
+            w.ept_obs.push_back(p->obs_list[i][1]);
+            const float invSigma2 = 1.0 / p->sigma_list[i];  // const float& (:6009)
+            w.ept_info.push_back((double)invSigma2);
+            w.ept_kfp.push_back(idx_all_kfs.at(kf_id));
+            w.ept_obs_idx.push_back((int)i);
+        }
+        w.maxPointId = id + 1;  // `if (maxPointId < id + 1);` — the condition is a no-op (:6025-6026)
+    }
+    // line vertices + edges (:6029-6117)
+    for (size_t li = 0; li < w.local_ls.size(); ++li) {
+        MapLine *l = w.local_ls[li];
+        const int id = l->idx + w.maxPointId + 1;
+        w.ln_id.push_back(id);
+        const Vec4 o = MapLine::changePlukerToOrth(l->NDw);
+        for (int k = 0; k < 4; ++k) w.ln_orth.push_back(o[k]);
+        for (size_t i = 0; i < l->kf_obs_list.size(); ++i) {
+            const int kf_id = l->kf_obs_list[i];
+            w.eln_lm.push_back((int32_t)li);
+            w.eln_kf.push_back(kf_pos.at(kf_id));
+            for (int k = 0; k < 4; ++k) w.eln_obs.push_back(l->NDw_obs_list[i][k]);
+            const float invSigma2 = 1.0 / l->sigma_list[i];  // (:6073)
+            w.eln_info.push_back((double)invSigma2);
+            w.eln_kfp.push_back(idx_all_kfs.at(kf_id));
+            w.eln_obs_idx.push_back((int)i);
+        }
+    }
+    // g2o::SparseOptimizer::addVertex refuses a duplicate id; refuse the window instead
+    std::vector<int32_t> ids(w.kf_id);
+    ids.insert(ids.end(), w.pt_id.begin(), w.pt_id.end());
+    ids.insert(ids.end(), w.ln_id.begin(), w.ln_id.end());
+    std::sort(ids.begin(), ids.end());
+    if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) {
+        setError("duplicate g2o vertex id in the window");
+        return PLBA_E_INVALID;
+    }
+    return PLBA_OK;
+}
+
+int MapHandler::solve(const plba_graph &g, plba_result &r) {
+    if (solve_fn_) {
+        const int rc = solve_fn_(solve_user_, &g, &r);
+        if (rc) setError("solver hook returned %d", rc);
+        return rc;
+    }
+    if (!ctx_) {
+        plba_opts o;
+        if (have_opts_) o = opts_;
+        else plba_default_opts(&o);
+        const int rc = plba_create(&ctx_, &o);
+        if (rc) {
+            setError("plba_create failed (%d): no usable MI355X device", rc);
+            ctx_ = nullptr;
+            return rc;
+        }
+    }
+    int rc = plba_upload(ctx_, &g);
+    if (!rc) rc = plba_lba_plucker(ctx_, &r);
+    if (rc) setError("plba: %s", plba_last_error(ctx_));
+    return rc;
+}
+
+// A1d: post-solve outlier bookkeeping (src/mapHandler.cpp:6154-6293), edges in reverse order.
+int MapHandler::outlierPass(Window &w, const std::vector<double> &ept_chi2, const std::vector<uint8_t> &ept_depth_ok,
+                            const std::vector<uint8_t> &ept_level, const std::vector<double> &eln_chi2,
+                            const std::vector<uint8_t> &eln_level, LbaStats &st) {
+    (void)ept_level;
+    (void)eln_level;  // level-1 errors were already refreshed by the solver (:6158-6160, 6226-6228)
+    auto graph_dec = [&](int a, int b) -> bool {
+        if (a < 0 || b < 0 || a >= (int)full_graph.size() || b >= (int)full_graph.size() ||
+            b >= (int)full_graph[a].size() || a >= (int)full_graph[b].size()) {
+            setError("full_graph has no entry (%d, %d)", a, b);
+            return false;
+        }
+        full_graph[a][b]--;  // unsigned, as the reference's vector<vector<unsigned int>>
+        full_graph[b][a]--;
+        return true;
+    };
+    // first observation removed: re-base the landmark (push only — the reference never erases
+    // it from the old KF's list; lines use map_points_kf_idx too, :6239-6251)
+    auto rebase = [&](int kf_obs, int lm_idx_map, int new_kf_base) -> bool {
+        auto it = map_points_kf_idx.find(kf_obs);
+        if (it == map_points_kf_idx.end()) {
+            setError("map_points_kf_idx.at(%d): no such key", kf_obs);
+            return false;
+        }
+        for (int v : it->second)
+            if (v == lm_idx_map) {
+                auto jt = map_points_kf_idx.find(new_kf_base);
+                if (jt == map_points_kf_idx.end()) {
+                    setError("map_points_kf_idx.at(%d): no such key", new_kf_base);
+                    return false;
+                }
+                jt->second.push_back(v);
+                break;
+            }
+        return true;
+    };
+
+    for (int i = (int)w.ept_lm.size() - 1; i >= 0; --i) {  // points (:6157-6214)
+        if (!(ept_chi2[i] > 5.991 || !ept_depth_ok[i])) continue;
+        st.bad_point_obs++;
+        KeyFrame *kf = w.ept_kfp[i];
+        MapPoint *pMP = w.local_pt[w.ept_lm[i]];
+        if (pMP->obs_list.size() > 1) {
+            st.actually_bad_point_obs++;
+            const int kf_obs = kf->kf_idx, lm_idx_map = pMP->idx, lm_idx_obs = w.ept_obs_idx[i];
+            if (lm_idx_obs == 0 && !rebase(kf_obs, lm_idx_map, pMP->kf_obs_list[1])) return PLBA_E_STATE;
+            pMP->desc_list.erase(pMP->desc_list.begin() + lm_idx_obs);
+            pMP->obs_list.erase(pMP->obs_list.begin() + lm_idx_obs);
+            pMP->dir_list.erase(pMP->dir_list.begin() + lm_idx_obs);
+            pMP->kf_obs_list.erase(pMP->kf_obs_list.begin() + lm_idx_obs);
+            for (int &f : kf->stereo_frame.stereo_pt_idx)
+                if (f == lm_idx_map) {
+                    f = -1;
+                    break;
+                }
+            pMP->updateAverageDescDir();
+            for (int idx : pMP->kf_obs_list)
+                if (kf_obs != idx && !graph_dec(kf_obs, idx)) return PLBA_E_STATE;
+        } else {
+            pMP->inlier = false;
+        }
+    }
+    for (int i = (int)w.eln_lm.size() - 1; i >= 0; --i) {  // lines (:6220-6288)
+        if (!(eln_chi2[i] > 5.991)) continue;
+        st.bad_line_obs++;
+        KeyFrame *kf = w.eln_kfp[i];
+        MapLine *lML = w.local_ls[w.eln_lm[i]];
+        if (lML->NDw_obs_list.size() > 1) {
+            st.actually_bad_line_obs++;
+            const int kf_obs = kf->kf_idx, lm_idx_map = lML->idx, lm_idx_obs = w.eln_obs_idx[i];
+            if (lm_idx_obs == 0 && !rebase(kf_obs, lm_idx_map, lML->kf_obs_list[1])) return PLBA_E_STATE;
+            lML->desc_list.erase(lML->desc_list.begin() + lm_idx_obs);
+            lML->NDw_obs_list.erase(lML->NDw_obs_list.begin() + lm_idx_obs);
+            lML->kf_obs_list.erase(lML->kf_obs_list.begin() + lm_idx_obs);
+            for (int &f : kf->stereo_frame.stereo_ls_idx)
+                if (f == lm_idx_map) {
+                    f = -1;
+                    break;
+                }
+            lML->updateAverageDescDir();
+            for (int idx : lML->kf_obs_list)
+                if (kf_obs != idx && !graph_dec(kf_obs, idx)) return PLBA_E_STATE;
+        } else {
+            lML->inlier = false;
+        }
+    }
+    return PLBA_OK;
+}
+
+int MapHandler::localBundleAdjustmentForPlukerWithG2O(LbaStats *stats) {
+    using clk = std::chrono::steady_clock;
+    LbaStats st;
+    const auto t0 = clk::now();
+    Window w;
+    int rc = gatherWindow(w);
+    if (rc) return rc;
+    const plba_graph g = w.graph(fx_, fy_, cx_, cy_);
+    st.n_free_kf = (int)w.nofix_kfs.size();
+    st.n_fixed_kf = (int)w.fix_kfs.size();
+    st.n_pt = g.n_pt; st.n_ln = g.n_ln; st.n_ept = g.n_ept; st.n_eln = g.n_eln;
+
+    std::vector<double> Tcw(w.kf_Tcw.size()), xyz(w.pt_xyz.size()), orth(w.ln_orth.size());
+    std::vector<double> ept_chi2(g.n_ept), eln_chi2(g.n_eln);
+    std::vector<uint8_t> ept_depth(g.n_ept), ept_level(g.n_ept), eln_level(g.n_eln);
+    plba_result r{};
+    r.kf_Tcw = Tcw.data(); r.pt_xyz = xyz.data(); r.ln_orth = orth.data();
+    r.ept_chi2 = ept_chi2.data(); r.ept_depth_ok = ept_depth.data(); r.ept_level = ept_level.data();
+    r.eln_chi2 = eln_chi2.data(); r.eln_level = eln_level.data();
+    const auto t1 = clk::now();
+    rc = solve(g, r);  // A1c (:6119-6152) on the device
+    if (rc) return rc;
+    const auto t2 = clk::now();
+    st.iters[0] = r.iters[0]; st.iters[1] = r.iters[1];
+    st.chi2[0] = r.chi2[0]; st.chi2[1] = r.chi2[1];
+    for (uint8_t l : eln_level) st.bad_line_stage1 += l == 1;  // "Bad Obs" (:6137-6147)
+
+    rc = outlierPass(w, ept_chi2, ept_depth, ept_level, eln_chi2, eln_level, st);
+    if (rc) return rc;
+
+    // A1e: write-back (:6296-6319). Free KFs (KF 0 included — it is in idx_nofix_kfs even though
+    // its vertex is fixed) get T_kf_w = estimate().inverse(); the vertex estimate is the 4x4
+    // inverse taken at graph build with R|t replaced by the solver's.
+    for (size_t k = 0; k < w.nofix_kfs.size(); ++k) {
+        KeyFrame *kf = w.nofix_kfs[k];
+        Mat4 est = inverse4(kf->T_kf_w);
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 4; ++b) est[a * 4 + b] = Tcw[k * 12 + a * 4 + b];
+        kf->T_kf_w = inverse4(est);
+    }
+    for (size_t p = 0; p < w.local_pt.size(); ++p)
+        for (int k = 0; k < 3; ++k) w.local_pt[p]->point3D[k] = xyz[p * 3 + k];
+    for (size_t l = 0; l < w.local_ls.size(); ++l) {
+        Vec4 o{orth[l * 4], orth[l * 4 + 1], orth[l * 4 + 2], orth[l * 4 + 3]};
+        w.local_ls[l]->NDw = MapLine::changeOrthToPluker(o);
+    }
+    const auto t3 = clk::now();
+    st.gather_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    st.solve_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    st.bookkeeping_ms = std::chrono::duration<double, std::milli>(t3 - t2).count();
+    if (stats) *stats = st;
+    return PLBA_OK;
+}
+
+}  // namespace plslam

@@ -1,0 +1,154 @@
+// Host-side mirror of the map state the Plücker LBA reads and mutates, and of
+// MapHandler::localBundleAdjustmentForPlukerWithG2O (src/mapHandler.cpp:5851-6323).
+//
+// The classes keep the reference's field names and list semantics (parallel per-observation
+// vectors, pointer vectors indexed by id, std::map<int, vector<int>> map_points_kf_idx,
+// vector<vector<unsigned>> full_graph) so the bookkeeping reads line-for-line against the
+// reference; Eigen/OpenCV types become fixed-size arrays (Matrix4d -> row-major double[16],
+// cv::Mat binary descriptor -> byte vector, NORM_HAMMING -> popcount).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "plba.h"
+
+namespace plslam {
+
+using Vec2 = std::array<double, 2>;
+using Vec3 = std::array<double, 3>;
+using Vec4 = std::array<double, 4>;
+using Vec6 = std::array<double, 6>;
+using Mat4 = std::array<double, 16>;  // row-major
+using Desc = std::vector<uint8_t>;
+
+// StVO::StereoFrame, reduced to what the LBA touches: the idx of each point / line feature
+// (src/mapHandler.cpp:6189-6198, 6262-6271).
+struct StereoFrame {
+    std::vector<int> stereo_pt_idx;
+    std::vector<int> stereo_ls_idx;
+};
+
+// include/keyFrame.h:50-71
+struct KeyFrame {
+    bool local = false;
+    int kf_idx = -1;
+    Mat4 T_kf_w{};  // camera -> world
+    StereoFrame stereo_frame;
+};
+
+// include/mapFeatures.h:39-66 and src/mapFeatures.cpp:38-94
+struct MapPoint {
+    int idx = -1;
+    bool inlier = true;
+    bool local = false;
+    Vec3 point3D{};
+    Vec3 med_obs_dir{};
+    Desc med_desc;
+    std::vector<Desc> desc_list;
+    std::vector<Vec2> obs_list;
+    std::vector<Vec3> dir_list;
+    std::vector<int> kf_obs_list;
+    std::vector<double> sigma_list;
+
+    MapPoint(int idx_, const Vec3 &p, const Desc &desc, int kf_obs, const Vec2 &obs, const Vec3 &dir, double sigma2);
+    void addMapPointObservation(const Desc &desc, int kf_obs, const Vec2 &obs, const Vec3 &dir, double sigma2);
+    void updateAverageDescDir();
+};
+
+// include/mapFeatures.h:68-107 (Plücker constructor, src/mapFeatures.cpp:114-138, 140-184
+// with USE_LINE_PLUKER: no direction average)
+struct MapLine {
+    int idx = -1;
+    bool inlier = true;
+    bool local = false;
+    Vec6 NDw{};
+    Desc med_desc;
+    std::vector<Desc> desc_list;
+    std::vector<Vec4> NDw_obs_list;
+    std::vector<int> kf_obs_list;
+    std::vector<double> sigma_list;
+
+    MapLine(int idx_, const Vec6 &NDw_, const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2);
+    void addMapLineObservation(const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2);
+    void updateAverageDescDir();
+
+    static Vec4 changePlukerToOrth(const Vec6 &L);
+    static Vec6 changeOrthToPluker(const Vec4 &o);
+};
+
+// Marshalled window: the plba_graph SoA arrays plus the back-references the outlier pass and
+// the write-back need (vpEdgeKFMono / vpMapPointEdgeMono / vpLmObsIdx, ...).
+struct Window {
+    std::vector<KeyFrame *> nofix_kfs, fix_kfs;  // idx_nofix_kfs / idx_fix_kfs in id order
+    std::vector<MapPoint *> local_pt;
+    std::vector<MapLine *> local_ls;
+    int max_kf_id = 0, maxPointId = 0;
+    // plba_graph arrays
+    std::vector<double> kf_Tcw, pt_xyz, ln_orth, ept_obs, ept_info, eln_obs, eln_info;
+    std::vector<uint8_t> kf_fixed;
+    std::vector<int32_t> kf_id, pt_id, ln_id, ept_lm, ept_kf, eln_lm, eln_kf;
+    // per-edge back references
+    std::vector<KeyFrame *> ept_kfp, eln_kfp;
+    std::vector<int> ept_obs_idx, eln_obs_idx;
+    plba_graph graph(double fx, double fy, double cx, double cy) const;
+};
+
+struct LbaStats {
+    int n_free_kf = 0, n_fixed_kf = 0, n_pt = 0, n_ln = 0, n_ept = 0, n_eln = 0;
+    int bad_line_stage1 = 0, bad_point_obs = 0, actually_bad_point_obs = 0, bad_line_obs = 0,
+        actually_bad_line_obs = 0;
+    int iters[2] = {0, 0};
+    double chi2[2] = {0, 0};
+    double gather_ms = 0, solve_ms = 0, bookkeeping_ms = 0;
+};
+
+using SolveFn = int (*)(void *user, const plba_graph *g, plba_result *r);
+
+// include/mapHandler.h:141-151 (the members the LBA uses)
+class MapHandler {
+  public:
+    MapHandler(double fx, double fy, double cx, double cy, const plba_opts *opts = nullptr);
+    ~MapHandler();
+    MapHandler(const MapHandler &) = delete;
+    MapHandler &operator=(const MapHandler &) = delete;
+
+    std::vector<KeyFrame *> map_keyframes;
+    std::vector<MapPoint *> map_points;
+    std::vector<MapLine *> map_lines;
+    std::map<int, std::vector<int>> map_points_kf_idx;
+    std::vector<std::vector<unsigned int>> full_graph;
+
+    // src/mapHandler.cpp:5851. Returns PLBA_OK or a PLBA_E_* status (the reference exit(0)s
+    // on an inconsistent map, :5894,5910,5998,6062; here the map is left untouched then).
+    int localBundleAdjustmentForPlukerWithG2O(LbaStats *stats = nullptr);
+
+    void setSolver(SolveFn fn, void *user) { solve_fn_ = fn; solve_user_ = user; }
+    const std::string &lastError() const { return err_; }
+    void setError(const char *fmt, ...);
+
+    // window gather + marshalling (A1, A1b) — public for tests
+    int gatherWindow(Window &w);
+
+  private:
+    int solve(const plba_graph &g, plba_result &r);
+    int outlierPass(Window &w, const std::vector<double> &ept_chi2, const std::vector<uint8_t> &ept_depth_ok,
+                    const std::vector<uint8_t> &ept_level, const std::vector<double> &eln_chi2,
+                    const std::vector<uint8_t> &eln_level, LbaStats &st);
+    double fx_, fy_, cx_, cy_;
+    plba_opts opts_{};
+    bool have_opts_ = false;
+    plba_ctx *ctx_ = nullptr;  // reused across LBA calls
+    SolveFn solve_fn_ = nullptr;
+    void *solve_user_ = nullptr;
+    std::string err_;
+};
+
+// helpers (host restatements)
+Mat4 inverse4(const Mat4 &T);  // Eigen Matrix4d::inverse (general cofactor inverse)
+int hamming(const Desc &a, const Desc &b);
+
+}  // namespace plslam
