@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "pl-slam-plucker_amd"))
 import numpy as np  # noqa: E402
 
 from plba import synth  # noqa: E402
+from plba.roofline import kernel_bytes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -47,29 +48,6 @@ def parse():
     p.add_argument("--cpu-runs", type=int, default=5)
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK (multi-rank rehearsal on 1 GPU)")
     return p.parse_args()
-
-
-def kernel_bytes(g: synth.Graph, name: str, d: dict) -> float:
-    """Algorithmic bytes one launch of `name` must move."""
-    E = g.n_ept + g.n_eln
-    n_lm = g.n_pt + g.n_ln
-    nf = int((g.kf_fixed == 0).sum())
-    bw = d.get("bw", 7)
-    band = nf * (bw + 1) * 36 * 8
-    if name == "k_rcs_factor":
-        # read band + b_s, write L band + S^-1 + z + x_p
-        return 2 * band + nf * (6 + 36 + 6 + 6) * 8
-    if name == "k_rcs_assemble":
-        # per triple: A1, A2 (12 f64 each), Z1, Z2 (8 each) + 2 i32 ; write the band
-        return d.get("triples", 0) * (40 * 8 + 8) + band
-    if name == "k_linearize":
-        # read state (T 12, X 4), obs 4, info, ids; write A 12, c 2, B 8, chi2
-        return E * ((12 + 4 + 4 + 1) * 8 + 12 + (12 + 2 + 8 + 1) * 8)
-    if name == "k_landmark_update":
-        return E * ((12 + 8 + 6 + 4 + 12) * 8 + 12) + n_lm * (10 + 4 + 4 + 4 + 4) * 8
-    if name == "k_schur_landmark":
-        return E * (8 + 8 + 2) * 8 + n_lm * (10 + 4 + 10 + 4) * 8
-    return 0.0
 
 
 def cpu_baseline(cfg: str, runs: int):
@@ -159,13 +137,23 @@ def main():
         info = s.structure_stats()
         alg = kernel_bytes(g, name, info)
         achieved = alg / (avg_ms * 1e-3) / 1e9
+        # rocprofv3 names the banded factorisation by its template (k_rcs_factor_band<BW>)
+        prof_name = "k_rcs_factor_band" if name == "k_rcs_factor" and info.get("banded") else name
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
         traffic = None
         if os.path.exists(pmc_path):
             try:
-                traffic = json.load(open(pmc_path)).get(name, {}).get("hbm_bytes_per_launch")
+                traffic = json.load(open(pmc_path)).get(prof_name, {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        per_kernel = {}
+        for k, (ms_k, n_k) in ktimes.items():
+            if n_k <= 0:
+                continue
+            b = kernel_bytes(g, k, info)
+            us = ms_k / n_k * 1e3
+            per_kernel[k] = {"us_per_launch": round(us, 2), "launches_per_lba": n_k,
+                             "alg_bytes": int(b), "GBs": round(b / (us * 1e-6) / 1e9, 1) if b else None}
         it_per_lba = tot_iters / max(a.steps * world, 1)
         iter_bytes = synth.algorithmic_bytes_per_iter(g)
         out = {
@@ -191,7 +179,7 @@ def main():
                 "parallelism": f"{world} independent windows (1 per GPU)",
             },
             "roofline": {
-                "kernel": name,
+                "kernel": prof_name,
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
@@ -208,7 +196,7 @@ def main():
                 "achieved_GBs": iter_bytes * (tot_iters / dt) / 1e9,
                 "frac": iter_bytes * (tot_iters / dt) / 1e9 / HBM_PEAK_GBS,
             },
-            "kernel_ms_per_lba": {k: round(v[0], 4) for k, v in ktimes.items()},
+            "kernels": per_kernel,
         }
         out["final_chi2_gpu"] = [float(r["chi2"][0]), float(r["chi2"][1])]
         if world == 1 and not a.no_cpu_baseline:

@@ -71,6 +71,7 @@ struct plba_ctx {
     std::vector<plba_iter_trace> trace;
     int stage = 0;
     size_t n_triples = 0;
+    int64_t n_free_edges = 0;  // edges whose pose vertex is free
     // captured step graph (one LM trial + guarded iteration / stage-switch work)
     hipGraph_t step_graph = nullptr;
     hipGraphExec_t step_exec = nullptr;
@@ -278,6 +279,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         e_info[pos] = g->eln_info[e];
     }
     for (int e = 0; e < E; ++e) e_hidx[e] = kf_hidx[e_kf[e]];
+    ctx->n_free_edges = std::count_if(e_hidx.begin(), e_hidx.end(), [](int32_t h) { return h >= 0; });
     ctx->e_orig = e_orig;
     ctx->h_level.assign(E, 0);
 
@@ -904,9 +906,9 @@ int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [16][8] */) {
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[7] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
-                          ctx->d.band_mode};
-    for (int i = 0; i < cap && i < 7; ++i) out[i] = v[i];
+    const int64_t v[10] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+                           ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep};
+    for (int i = 0; i < cap && i < 10; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

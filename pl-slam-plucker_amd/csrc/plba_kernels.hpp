@@ -7,14 +7,21 @@
 //   k_landmark_reduce  landmark-parallel: Hll, b_l; max|diag| partials
 //   k_iter_init        χ²_cur, λ init (τ·max|H_jj|, iteration 0)
 // Stage switch (initializeOptimization): k_switch_classify / _clear / _activate / _finish.
-// Per damped trial:
-//   k_schur_landmark   (Hll+λI) = LLᵀ per landmark; Z_e = B_e L⁻ᵀ, q_e = Z_e L⁻¹ b_l
-//   k_rcs_assemble     one wave per reduced-camera block: Hpp+λI − Σ A₁ᵀ(Z₁Z₂ᵀ)A₂ ; b_s
-//   k_rcs_factor       one workgroup: envelope-aware tiled LDLᵀ + solve (LinearSolverEigen)
-//   k_pose_update      oplus of the free poses, scale partials
-//   k_landmark_update  back-substitution, oplus, trial χ² of every active edge
-//   k_decide           ρ, accept/reject, λ/ν update (g2o Levenberg rules)
+// Per damped trial (TRIAL_GUARD):
+//   k_lm_chol          landmark-parallel: (Hll+λI) = LLᵀ, g = L⁻¹ b_l
+//   k_edge_schur       edge-parallel: Z_e = B_e L⁻ᵀ, q_e = Z_e g
+//   k_rcs_chunk        one wave per chunk of <=128 (e1,e2) triples of one RCS block:
+//                      Σ A₁ᵀ(Z₁Z₂ᵀ)A₂ (and Σ A_eᵀq_e on diagonal blocks)
+//   k_rcs_finalize     per block entry: Hpp+λI − Σ chunks into the band (or dense) matrix, b_s
+//   k_rcs_factor_band<BW>  one workgroup: block-banded LDLᵀ + forward/backward solve
+//                      (LinearSolverEigen); k_rcs_factor is the dense-envelope fallback (bw>20)
+//   k_pose_update      oplus of the free poses, pose part of Σx(λx+b)
+//   k_edge_backsub     edge-parallel: u_e = B_eᵀ A_e x_p
+//   k_lm_solve         landmark-parallel: x_l = L⁻ᵀL⁻¹(b_l − Σu_e), oplus, Σx(λx+b) partials
+//   k_edge_eval        edge-parallel: χ² at the trial state, robust partial sums
+//   k_decide           ρ, accept/reject, λ/ν update, optimize() loop control (g2o Levenberg)
 //   k_commit           trial -> current on accept (push/pop/discardTop)
+// After the schedule: k_refresh (level-1 computeError) and k_depth (isDepthPositive).
 // All reductions are fixed-order trees: results are bitwise reproducible run to run.
 #pragma once
 

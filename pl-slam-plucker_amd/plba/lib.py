@@ -195,9 +195,10 @@ class Solver:
         return {names[i].decode(): (float(ms[i]), int(nl[i])) for i in range(n.value)}
 
     def structure_stats(self) -> dict:
-        st = (C.c_int64 * 8)()
-        self._check(self.L.plba_structure_stats(self.ctx, st, 8), "plba_structure_stats")
-        return dict(nf=st[0], bw=st[1], nblk=st[2], triples=st[3], edges=st[4], landmarks=st[5], banded=st[6])
+        st = (C.c_int64 * 10)()
+        self._check(self.L.plba_structure_stats(self.ctx, st, 10), "plba_structure_stats")
+        return dict(nf=st[0], bw=st[1], nblk=st[2], triples=st[3], edges=st[4], landmarks=st[5], banded=st[6],
+                    chunks=st[7], free_edges=st[8], point_edges=st[9])
 
     def synchronize(self):
         self._check(self.L.plba_synchronize(self.ctx), "plba_synchronize")

@@ -1,0 +1,63 @@
+"""Algorithmic bytes per kernel launch: the bytes a launch must move at
+minimum — each input array read once, each output written once, per-landmark / per-pose
+state counted once (not once per edge). Re-reads through L2/MALL and padding are *not*
+counted; PMC traffic above these figures is waste.
+
+Units (f64 = 8 B, index = 4 B), with E = E_p + E_l, E_f = edges whose pose is free,
+n_lm = N_p + N_l, nf = free poses, T = Schur triples, nblk = RCS blocks, nch = chunks,
+bw = envelope bandwidth in pose blocks.
+"""
+from __future__ import annotations
+
+from .synth import Graph
+
+F = 8
+I = 4
+
+
+def state_bytes(g: Graph) -> int:
+    """pose (12 f64), point (3 f64), line orth (4 f64) — read once."""
+    return g.n_kf * 12 * F + g.n_pt * 3 * F + g.n_ln * 4 * F
+
+
+def kernel_bytes(g: Graph, name: str, st: dict) -> float:
+    E, Ep, El = g.n_ept + g.n_eln, g.n_ept, g.n_eln
+    Ef = st.get("free_edges", E)
+    n_lm = g.n_pt + g.n_ln
+    nf = st.get("nf", int((g.kf_fixed == 0).sum()))
+    bw = st.get("bw", 7)
+    T = st.get("triples", 0)
+    nblk = st.get("nblk", 0)
+    nch = st.get("chunks", 0)
+    blk = 36 * F
+    if name == "k_linearize":
+        # read: 2 indices, obs (2|4 f64), info, active flag, pose index; states once
+        # write: A (12), c (2), B (8), χ² (1) per edge
+        rd = Ep * (2 * I + 2 * F + F + 1 + I) + El * (2 * I + 4 * F + F + 1 + I) + state_bytes(g)
+        return rd + E * (12 + 2 + 8 + 1) * F
+    if name == "k_pose_reduce":
+        return Ef * (I + 14 * F) + nf * (36 + 6 + 1) * F
+    if name == "k_landmark_reduce":
+        return E * (8 + 2) * F + n_lm * (I + (10 + 4) * F)
+    if name == "k_lm_chol":
+        return n_lm * (10 + 4 + 10 + 4) * F
+    if name == "k_edge_schur":
+        return E * (I + 8 * F + 10 * F) + n_lm * (10 + 4) * F
+    if name == "k_rcs_chunk":
+        # every edge's A (12) and Z (8), q (2) read once; the triple list; 42 partials per chunk
+        return E * (12 + 8 + 2) * F + T * 2 * I + nch * 42 * F
+    if name == "k_rcs_finalize":
+        return nch * 42 * F + nf * (36 + 6) * F + nblk * blk + nf * 6 * F
+    if name in ("k_rcs_factor", "k_rcs_factor_band"):
+        # band in (nf·(bw+1) blocks) + b_s; L band, S⁻¹, z, x_p out
+        return nf * (bw + 1) * blk + nf * 6 * F + nf * bw * blk + nf * (36 + 6 + 6) * F
+    if name == "k_pose_update":
+        return g.n_kf * (12 + 12) * F + nf * 12 * F
+    if name == "k_edge_backsub":
+        return Ef * (I + (12 + 8) * F) + nf * 6 * F + E * 4 * F
+    if name == "k_lm_solve":
+        return n_lm * (4 + 4 + 10 + 4 + 4) * F + n_lm * I + E * 4 * F + g.n_ln * 6 * F
+    if name == "k_edge_eval":
+        rd = Ep * (2 * I + 2 * F + F + 1) + El * (2 * I + 4 * F + F + 1)
+        return rd + g.n_kf * 12 * F + g.n_pt * 3 * F + g.n_ln * 6 * F + E * F
+    return 0.0
