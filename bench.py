@@ -8,9 +8,14 @@ window: reset estimates -> optimize(5) with Huber -> outlier classification -> o
 wall time. Workload (N=1): config C3 = 100 KF / 20k points / 4k lines (BASELINE.json
 configs[2], the window north_star quotes its ≥50x target on).
 
-Multi-GPU (`--gpus N`, launched by torch.distributed.run): every rank solves its own
-independent C3 window (different seed) — independent LBA windows shard with no data-path
-collective (weak scaling); the barrier and max-over-ranks timing use torch.distributed.
+Multi-GPU (`--gpus N`, launched by torch.distributed.run), two modes:
+  --mode replicas (default)  every rank solves its own independent C3 window (different seed):
+                             independent LBA windows need no data-path collective (weak scaling).
+  --mode shard               ONE window (default C4) split over the ranks by landmark
+                             (SURVEY.md §8e), partial reduced camera systems summed with RCCL
+                             all-reduces inside the captured step graph (strong scaling);
+                             `--transport host` rehearses it with gloo on one GPU.
+The barrier and max-over-ranks timing use torch.distributed in both.
 
 Extra JSON objects:
   roofline      dominant kernel (by device time), algorithmic bytes per launch / avg launch
@@ -47,6 +52,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-runs", type=int, default=5)
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK (multi-rank rehearsal on 1 GPU)")
+    p.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
+    p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="--mode shard all-reduce transport")
     return p.parse_args()
 
 
@@ -86,9 +93,26 @@ def main():
         dist.init_process_group("gloo")
     from plba.lib import Solver
 
+    shard = a.mode == "shard"
+    if shard and a.config == "C3" and "--config" not in sys.argv:
+        a.config = "C4"
     base_seed = synth.CONFIGS[a.config][3]
-    g = synth.generate(a.config, seed=base_seed + 97 * rank)
-    s = Solver(device=local if a.device is None else a.device)
+    dev = local if a.device is None else a.device
+    if shard:  # one window for all ranks
+        g = synth.generate(a.config, seed=base_seed)
+        if dist is None:
+            from plba.lib import comm_unique_id
+            s = Solver(device=dev)
+            if a.transport == "rccl":
+                s.comm_init_rccl(1, 0, comm_unique_id())
+            else:
+                s.comm_init_host(1, 0, lambda buf: None)
+        else:
+            from plba.dist import sharded_solver
+            s = sharded_solver(device=dev, transport=a.transport)
+    else:
+        g = synth.generate(a.config, seed=base_seed + 97 * rank)
+        s = Solver(device=dev)
     t0 = time.perf_counter()
     s.upload(g)
     s.synchronize()
@@ -126,9 +150,10 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-        ti = torch.tensor([iters], dtype=torch.float64)
-        dist.all_reduce(ti, op=dist.ReduceOp.SUM)
-        tot_iters = int(ti.item())
+        if not shard:  # replicas: every rank's iterations count; shard: one window's
+            ti = torch.tensor([iters], dtype=torch.float64)
+            dist.all_reduce(ti, op=dist.ReduceOp.SUM)
+            tot_iters = int(ti.item())
 
     if rank == 0:
         # dominant kernel by device time in the instrumented step
@@ -154,7 +179,7 @@ def main():
             us = ms_k / n_k * 1e3
             per_kernel[k] = {"us_per_launch": round(us, 2), "launches_per_lba": n_k,
                              "alg_bytes": int(b), "GBs": round(b / (us * 1e-6) / 1e9, 1) if b else None}
-        it_per_lba = tot_iters / max(a.steps * world, 1)
+        it_per_lba = tot_iters / max(a.steps * (1 if shard else world), 1)
         iter_bytes = synth.algorithmic_bytes_per_iter(g)
         out = {
             "metric": "LM iterations/sec (and ms/iter) on local-BA window; final \u03c7\u00b2 vs g2o",
@@ -165,18 +190,21 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded EuRoC-shaped window, SURVEY.md §8d)",
             "config": {
                 "workload": f"{a.config}: {g.n_kf} KF ({int(g.kf_fixed.sum())} fixed) / {g.n_pt} points / "
-                            f"{g.n_ln} Plücker lines, {g.n_ept}+{g.n_eln} edges; one independent window per GPU",
+                            f"{g.n_ln} Plücker lines, {g.n_ept}+{g.n_eln} edges; "
+                            + (f"one window sharded over {world} GPU(s) by landmark ({a.transport} all-reduce)"
+                               if shard else "one independent window per GPU"),
                 "lm_iterations_per_lba": it_per_lba,
                 "trials_per_lba": trials / a.steps,
-                "ms_per_lm_iteration": dt / max(iters, 1) * 1e3 if world == 1 else dt / (tot_iters / world) * 1e3,
+                "ms_per_lm_iteration": dt / max(iters, 1) * 1e3,
                 "upload_ms": upload_ms,
-                "parallelism": f"{world} independent windows (1 per GPU)",
+                "parallelism": (f"landmark-sharded window over {world} GPU(s)" if shard
+                                else f"{world} independent windows (1 per GPU)"),
             },
             "roofline": {
                 "kernel": prof_name,
@@ -201,7 +229,7 @@ def main():
         out["final_chi2_gpu"] = [float(r["chi2"][0]), float(r["chi2"][1])]
         if world == 1 and not a.no_cpu_baseline:
             try:
-                cb = cpu_baseline(a.config, a.cpu_runs)
+                cb = cpu_baseline(a.config, a.cpu_runs if a.config in ("C1", "C1L", "C2", "C3") else 1)
                 out["final_chi2_cpu"] = cb.pop("final_chi2")
                 out["final_chi2_rel_diff"] = max(abs(x - y) / abs(y) for x, y in
                                                  zip(out["final_chi2_gpu"], out["final_chi2_cpu"]))

@@ -135,10 +135,33 @@ int plba_synchronize(plba_ctx *ctx);
 int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on);   /* HIP-event timing of each launch */
 /* Structure of the uploaded window: out[0]=free poses, [1]=envelope bandwidth (pose blocks),
  * [2]=reduced-camera blocks, [3]=Schur triples, [4]=edges, [5]=landmarks, [6]=banded (1/0),
- * [7]=assembly chunks, [8]=edges with a free pose, [9]=point edges. */
+ * [7]=assembly chunks, [8]=edges with a free pose, [9]=point edges, [10]=step hipGraph in use,
+ * [11]=sharded code path. Counts are this rank's when the window is sharded. */
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap);
 int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,
                       int32_t cap, int32_t *n);
+
+/* ---- Sharded windows: one context per GPU, one window split over nranks.
+ * Landmarks (with all their edges) are partitioned by the keyframe range of their first
+ * observation (kf_obs_list[0], the base KF of map_points_kf_idx); poses are replicated.
+ * Per LM trial each rank assembles its partial reduced camera system and the ranks sum it
+ * with one all-reduce (plus a 42·nf-double all-reduce per outer iteration and a 2-double one
+ * per trial); every rank then factorises the identical system redundantly, so accept/reject
+ * decisions agree bit for bit across ranks. plba_download / plba_get_edge_chi2 /
+ * plba_lba_plucker return the FULL window on every rank (one final gather all-reduce).
+ * Call exactly one plba_comm_init_* before plba_upload; every rank uploads the same full
+ * graph and then makes the same sequence of calls. */
+
+/* In-place sum over ranks of n doubles in host memory (caller's transport, e.g. gloo). */
+typedef int (*plba_host_allreduce_fn)(void *user, double *buf, int64_t n);
+
+/* Landmark -> rank assignment used by sharded uploads (pure host code, no device needed). */
+int plba_shard_plan(const plba_graph *g, int32_t nranks, int32_t *pt_owner, int32_t *ln_owner);
+/* RCCL transport over xGMI: rank 0 creates the id, the caller broadcasts its 128 bytes. */
+int plba_comm_unique_id(uint8_t id[128]);
+int plba_comm_init_rccl(plba_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+/* Host transport (tests / hosts without RCCL): device buffers are staged through pinned memory. */
+int plba_comm_init_host(plba_ctx *ctx, int32_t nranks, int32_t rank, plba_host_allreduce_fn fn, void *user);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,7 @@
 // The numerical work is all on the device (plba_kernels.hpp); the host only reads back the
 // 80-byte control block after each trial to decide whether another trial runs.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -60,6 +61,16 @@ struct plba_ctx {
     int level = 0;
     int robust = 1;
     Dev d{};
+    // sharded windows: transport of the three per-step all-reduces
+    struct Comm {
+        enum Kind { NONE, RCCL, HOST } kind = NONE;
+        int nranks = 1, rank = 0;
+        ncclComm_t nccl = nullptr;
+        plba_host_allreduce_fn fn = nullptr;
+        void *user = nullptr;
+        double *hbuf = nullptr;  // pinned staging (HOST)
+        size_t hcap = 0;
+    } comm;
     // device arena
     std::vector<void *> allocs;
     Ctrl *h_ctrl = nullptr;  // pinned
@@ -76,6 +87,7 @@ struct plba_ctx {
     hipGraph_t step_graph = nullptr;
     hipGraphExec_t step_exec = nullptr;
     int last_steps = 16;     // steps the previous schedule needed (first batch size)
+    bool no_graph = false;   // set when the step cannot be captured (RCCL without capture support)
     int steps_launched = 0;
     // kernel timing (optional)
     bool timing = false;
@@ -135,6 +147,40 @@ struct plba_ctx {
 namespace {
 
 inline int blocks_for(int n, int b = kBlock) { return (n + b - 1) / b; }
+
+// Landmark -> rank: landmarks ordered by the id rank of the keyframe of their
+// first observation (kf_obs_list[0]), cut into nranks contiguous runs of ~equal edge count.
+void shard_plan(const plba_graph *g, int R, int32_t *pt_owner, int32_t *ln_owner) {
+    std::vector<int32_t> korder(g->n_kf), kpos(g->n_kf);
+    std::iota(korder.begin(), korder.end(), 0);
+    std::stable_sort(korder.begin(), korder.end(), [&](int a, int b) { return g->kf_id[a] < g->kf_id[b]; });
+    for (int i = 0; i < g->n_kf; ++i) kpos[korder[i]] = i;
+    const int np = g->n_pt, nl = g->n_ln;
+    std::vector<int32_t> key(np + nl, INT32_MAX), cnt(np + nl, 0);
+    for (int e = 0; e < g->n_ept; ++e) {
+        const int l = g->ept_lm[e];
+        if (cnt[l]++ == 0) key[l] = kpos[g->ept_kf[e]];
+    }
+    for (int e = 0; e < g->n_eln; ++e) {
+        const int l = np + g->eln_lm[e];
+        if (cnt[l]++ == 0) key[l] = kpos[g->eln_kf[e]];
+    }
+    std::vector<int32_t> ord(np + nl);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key[a] < key[b]; });
+    int64_t total = 0, acc = 0;
+    for (int c : cnt) total += c;
+    for (int l : ord) {
+        // rank of this landmark's edge-count midpoint
+        const int64_t mid2 = 2 * acc + cnt[l];
+        int r = total > 0 ? (int)((mid2 * R) / (2 * total)) : 0;
+        r = std::min(std::max(r, 0), R - 1);
+        acc += cnt[l];
+        if (l < np) pt_owner[l] = r;
+        else ln_owner[l - np] = r;
+    }
+}
+
 inline size_t band_lds_bytes(int bw) {
     const size_t W = bw + 1;
     return sizeof(double) * (W * W * 36 + W * 6 + W * 36 + 72 + W * 6 + W * 6 + 12);
@@ -239,9 +285,23 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             return PLBA_E_INVALID;
         }
     ctx->free_all();
-    const int n_kf = g->n_kf, n_pt = g->n_pt, n_ln = g->n_ln, Ep = g->n_ept, El = g->n_eln;
+    const int n_kf = g->n_kf, n_pt_g = g->n_pt, n_ln_g = g->n_ln, Ep_g = g->n_ept, El_g = g->n_eln;
+    const int R = ctx->comm.nranks, rank = ctx->comm.rank;
+    ctx->n_kf = n_kf; ctx->n_pt = n_pt_g; ctx->n_ln = n_ln_g; ctx->Ep = Ep_g; ctx->El = El_g;
+
+    // landmarks owned by this rank (all of them unless the window is sharded)
+    std::vector<int32_t> pt_owner(n_pt_g, 0), ln_owner(n_ln_g, 0);
+    if (R > 1) shard_plan(g, R, pt_owner.data(), ln_owner.data());
+    std::vector<int32_t> pt_loc(n_pt_g, -1), ln_loc(n_ln_g, -1), lm_gpos;
+    int n_pt = 0, n_ln = 0;
+    for (int p = 0; p < n_pt_g; ++p)
+        if (pt_owner[p] == rank) { pt_loc[p] = n_pt++; lm_gpos.push_back(p); }
+    for (int l = 0; l < n_ln_g; ++l)
+        if (ln_owner[l] == rank) { ln_loc[l] = n_ln++; lm_gpos.push_back(n_pt_g + l); }
+    int Ep = 0, El = 0;
+    for (int e = 0; e < Ep_g; ++e) Ep += pt_loc[g->ept_lm[e]] >= 0;
+    for (int e = 0; e < El_g; ++e) El += ln_loc[g->eln_lm[e]] >= 0;
     const int n_lm = n_pt + n_ln, E = Ep + El;
-    ctx->n_kf = n_kf; ctx->n_pt = n_pt; ctx->n_ln = n_ln; ctx->Ep = Ep; ctx->El = El;
 
     // free poses ordered by vertex id (buildIndexMapping)
     std::vector<int32_t> korder(n_kf);
@@ -252,29 +312,36 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     for (int k : korder)
         if (!g->kf_fixed[k]) kf_hidx[k] = nf++;
 
-    // landmark-major CSR (stable within a landmark = g2o insertion order)
+    // landmark-major CSR of the local landmarks (stable within a landmark = g2o insertion order)
     std::vector<int32_t> lm_cnt(n_lm + 1, 0);
-    for (int e = 0; e < Ep; ++e) lm_cnt[g->ept_lm[e] + 1]++;
-    for (int e = 0; e < El; ++e) lm_cnt[n_pt + g->eln_lm[e] + 1]++;
+    for (int e = 0; e < Ep_g; ++e)
+        if (pt_loc[g->ept_lm[e]] >= 0) lm_cnt[pt_loc[g->ept_lm[e]] + 1]++;
+    for (int e = 0; e < El_g; ++e)
+        if (ln_loc[g->eln_lm[e]] >= 0) lm_cnt[n_pt + ln_loc[g->eln_lm[e]] + 1]++;
     std::vector<int32_t> lm_off(n_lm + 1, 0);
     for (int l = 0; l < n_lm; ++l) lm_off[l + 1] = lm_off[l] + lm_cnt[l + 1];
     std::vector<int32_t> fill(lm_off.begin(), lm_off.end() - 1);
-    std::vector<int32_t> e_lm(E), e_kf(E), e_hidx(E), e_orig(E);
+    std::vector<int32_t> e_lm(E), e_kf(E), e_hidx(E), e_orig(E), e_gpos(E);
     std::vector<double> e_obs((size_t)E * 4, 0.0), e_info(E);
-    for (int e = 0; e < Ep; ++e) {
-        int l = g->ept_lm[e], pos = fill[l]++;
+    for (int e = 0; e < Ep_g; ++e) {
+        const int l = pt_loc[g->ept_lm[e]];
+        if (l < 0) continue;
+        const int pos = fill[l]++;
         e_lm[pos] = l;
         e_kf[pos] = g->ept_kf[e];
         e_orig[pos] = e;
+        e_gpos[pos] = e;
         e_obs[(size_t)pos * 4] = g->ept_obs[2 * e];
         e_obs[(size_t)pos * 4 + 1] = g->ept_obs[2 * e + 1];
         e_info[pos] = g->ept_info[e];
     }
-    for (int e = 0; e < El; ++e) {
-        int l = n_pt + g->eln_lm[e], pos = fill[l]++;
+    for (int e = 0; e < El_g; ++e) {
+        if (ln_loc[g->eln_lm[e]] < 0) continue;
+        const int l = n_pt + ln_loc[g->eln_lm[e]], pos = fill[l]++;
         e_lm[pos] = l;
         e_kf[pos] = g->eln_kf[e];
         e_orig[pos] = e;
+        e_gpos[pos] = Ep_g + e;
         for (int k = 0; k < 4; ++k) e_obs[(size_t)pos * 4 + k] = g->eln_obs[4 * e + k];
         e_info[pos] = g->eln_info[e];
     }
@@ -295,14 +362,34 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             if (e_hidx[e] >= 0) pe_list[f[e_hidx[e]]++] = e;
     }
 
-    // reduced-camera block pattern + triples (e1 at pose i1 <= e2 at pose i2, same landmark)
+    // reduced-camera block pattern + triples (e1 at pose i1 <= e2 at pose i2, same landmark).
+    // The pattern is that of the WHOLE window on every rank (the all-reduced value array must
+    // have one layout); triples come from the local landmarks only.
     std::map<std::pair<int, int>, int> blk_index;
     std::vector<std::pair<int, int>> blocks;
-    for (int h = 0; h < nf; ++h) {
-        blk_index[{h, h}] = (int)blocks.size();
-        blocks.push_back({h, h});
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> blk_trip;
+    auto block_of = [&](int i1, int i2) {
+        auto key = std::make_pair(i1, i2);
+        auto it = blk_index.find(key);
+        if (it != blk_index.end()) return it->second;
+        const int bi = (int)blocks.size();
+        blk_index[key] = bi;
+        blocks.push_back(key);
+        blk_trip.emplace_back();
+        return bi;
+    };
+    for (int h = 0; h < nf; ++h) block_of(h, h);
+    if (R > 1) {  // global pattern: free poses observing each landmark of the full window
+        std::vector<std::vector<int32_t>> obs_h(n_pt_g + n_ln_g);
+        for (int e = 0; e < Ep_g; ++e)
+            if (kf_hidx[g->ept_kf[e]] >= 0) obs_h[g->ept_lm[e]].push_back(kf_hidx[g->ept_kf[e]]);
+        for (int e = 0; e < El_g; ++e)
+            if (kf_hidx[g->eln_kf[e]] >= 0) obs_h[n_pt_g + g->eln_lm[e]].push_back(kf_hidx[g->eln_kf[e]]);
+        for (auto &hs : obs_h)
+            for (int a : hs)
+                for (int b : hs)
+                    if (a < b) block_of(a, b);
     }
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> blk_trip(nf);
     std::vector<int32_t> lm_edges;
     for (int l = 0; l < n_lm; ++l) {
         lm_edges.clear();
@@ -310,20 +397,9 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             if (e_hidx[e] >= 0) lm_edges.push_back(e);
         for (int a : lm_edges)
             for (int b : lm_edges) {
-                int i1 = e_hidx[a], i2 = e_hidx[b];
+                const int i1 = e_hidx[a], i2 = e_hidx[b];
                 if (i1 > i2) continue;
-                auto key = std::make_pair(i1, i2);
-                auto it = blk_index.find(key);
-                int bi;
-                if (it == blk_index.end()) {
-                    bi = (int)blocks.size();
-                    blk_index[key] = bi;
-                    blocks.push_back(key);
-                    blk_trip.emplace_back();
-                } else {
-                    bi = it->second;
-                }
-                blk_trip[bi].push_back({a, b});
+                blk_trip[block_of(i1, i2)].push_back({a, b});
             }
     }
     // envelope (first block column per block row) and bandwidth
@@ -400,6 +476,13 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     Dev &d = ctx->d;
     d.n_kf = n_kf; d.n_pt = n_pt; d.n_ln = n_ln; d.n_lm = n_lm; d.Ep = Ep; d.El = El; d.E = E;
     d.nf = nf; d.n = n; d.nblk = nblk; d.ntiles = ntiles;
+    // any transport selects the sharded code path (a 1-rank RCCL window exercises it on one GPU)
+    const bool sharded = ctx->comm.kind != plba_ctx::Comm::NONE;
+    d.sharded = sharded ? 1 : 0;
+    d.nranks = R;
+    d.rank = rank;
+    d.n_lm_g = n_pt_g + n_ln_g;
+    d.E_g = Ep_g + El_g;
     d.bw = bw;
     d.band_mode = band_mode ? 1 : 0;
     d.ring = band_ring(bw, nf);
@@ -415,9 +498,10 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     std::vector<double> T((size_t)n_kf * 12), X((size_t)n_lm * 4, 0.0);
     for (size_t i = 0; i < T.size(); ++i) T[i] = g->kf_Tcw[i];
     for (int p = 0; p < n_pt; ++p)
-        for (int k = 0; k < 3; ++k) X[(size_t)p * 4 + k] = g->pt_xyz[3 * p + k];
+        for (int k = 0; k < 3; ++k) X[(size_t)p * 4 + k] = g->pt_xyz[3 * (size_t)lm_gpos[p] + k];
     for (int l = 0; l < n_ln; ++l)
-        for (int k = 0; k < 4; ++k) X[(size_t)(n_pt + l) * 4 + k] = g->ln_orth[4 * l + k];
+        for (int k = 0; k < 4; ++k)
+            X[(size_t)(n_pt + l) * 4 + k] = g->ln_orth[4 * (size_t)(lm_gpos[n_pt + l] - n_pt_g) + k];
 
     int rc = 0;
 #define ALLOC(p, n_)        \
@@ -449,8 +533,17 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.cvec, (size_t)E * 2);
     ALLOC(d.B, (size_t)E * 8);
     ALLOC(d.chi2_last, E);
-    ALLOC(d.Hpp, (size_t)nf * 36);
-    ALLOC(d.bp, (size_t)nf * 6);
+    // Hpp | b_p | χ² | active | landmark max per rank: one array, all-reduced when sharded
+    ALLOC(d.red_iter, (size_t)nf * 42 + 2 + R);
+    d.Hpp = d.red_iter;
+    d.bp = d.red_iter + (size_t)nf * 36;
+    if (sharded) {
+        ALLOC(d.red_iter_loc, (size_t)nf * 42 + 2 + R);
+    } else {
+        d.red_iter_loc = d.red_iter;
+    }
+    d.Hpp_w = d.red_iter_loc;
+    d.bp_w = d.red_iter_loc + (size_t)nf * 36;
     ALLOC(d.Hll, (size_t)n_lm * 10);
     ALLOC(d.bl, (size_t)n_lm * 4);
     ALLOC(d.Lc, (size_t)n_lm * 10);
@@ -488,6 +581,17 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.ctrl, 1);
     ALLOC(d.trace, kTraceCap);
     ALLOC(ctx->d_depth, Ep);
+    ALLOC(d.red_rcs, (size_t)nblk * 36 + (size_t)nf * 6);
+    ALLOC(d.red_dec, 2);
+    if (sharded) {
+        ALLOC(d.red_rcs_loc, (size_t)nblk * 36 + (size_t)nf * 6);
+        ALLOC(d.red_dec_loc, 2);
+    }
+    if (sharded) {  // final gather of the full window: X | χ² | depth | level
+        UPLOAD(d.lm_gpos, lm_gpos);
+        UPLOAD(d.e_gpos, e_gpos);
+        ALLOC(d.gat, (size_t)(n_pt_g + n_ln_g) * 4 + 3 * (size_t)(Ep_g + El_g));
+    }
 #ifdef PLBA_STAMPS
     ALLOC(d.stamps, 16 * 8);
     PLBA_CHECK(hipMemset(d.stamps, 0, 16 * 8 * sizeof(unsigned long long)));
@@ -514,6 +618,44 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 // One "step": [stage switch] -> [iteration: linearise + reductions + λ init] -> one damped
 // trial -> decide -> commit. Every kernel is guarded by the device control block, so a fixed
 // sequence can be captured once and replayed; steps after the schedule finished are no-ops.
+// Sum of n doubles over the ranks of a sharded window: send (this rank's partials) -> recv.
+int allreduce(plba_ctx *ctx, const double *send, double *recv, size_t n) {
+    auto &c = ctx->comm;
+    if (n == 0) return PLBA_OK;
+    if (c.kind == plba_ctx::Comm::RCCL) {
+        const ncclResult_t r = ncclAllReduce(send, recv, n, ncclDouble, ncclSum, c.nccl, ctx->stream);
+        if (r != ncclSuccess) {
+            ctx->set_error("ncclAllReduce(%zu doubles): %s", n, ncclGetErrorString(r));
+            return PLBA_E_COMM;
+        }
+        return PLBA_OK;
+    }
+    if (c.kind == plba_ctx::Comm::HOST) {
+        if (c.hcap < n) {
+            if (c.hbuf) (void)hipHostFree(c.hbuf);
+            c.hbuf = nullptr;
+            PLBA_CHECK(hipHostMalloc((void **)&c.hbuf, n * sizeof(double), hipHostMallocDefault));
+            c.hcap = n;
+        }
+        PLBA_CHECK(hipMemcpyAsync(c.hbuf, send, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+        const int rc = c.fn(c.user, c.hbuf, (int64_t)n);
+        if (rc) {
+            ctx->set_error("host all-reduce callback returned %d", rc);
+            return PLBA_E_COMM;
+        }
+        PLBA_CHECK(hipMemcpyAsync(recv, c.hbuf, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+        return PLBA_OK;
+    }
+    ctx->set_error("sharded window without a transport");
+    return PLBA_E_COMM;
+}
+#define COMM(send, recv, n)                                  \
+    do {                                                     \
+        int _rc = allreduce(ctx, (send), (recv), (size_t)(n)); \
+        if (_rc) return _rc;                                 \
+    } while (0)
+
 int launch_step(plba_ctx *ctx) {
     Dev &d = ctx->d;
     hipStream_t s = ctx->stream;
@@ -527,6 +669,10 @@ int launch_step(plba_ctx *ctx) {
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+    if (d.sharded) {
+        LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kBlock), 0, s, d));
+        COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 42 + 2 + d.nranks);
+    }
     LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) {
         LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_lm_chol, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
@@ -535,6 +681,10 @@ int launch_step(plba_ctx *ctx) {
     if (d.n > 0) {
         if (!d.band_mode) LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
         if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_chunk, dim3(d.nch), dim3(64), 0, s, d));
+        if (d.sharded) {
+            LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
+            COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);
+        }
         LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
         if (d.band_mode) LAUNCH(K_FACTOR, launch_band(d, band_lds_bytes(d.bw, d.nf), s));
         else LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
@@ -544,6 +694,10 @@ int launch_step(plba_ctx *ctx) {
         LAUNCH(K_BACKSUB, hipLaunchKernelGGL(k_edge_backsub, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
         LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
         LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+    }
+    if (d.sharded) {
+        LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide_pack, dim3(1), dim3(kBlock), 0, s, d));
+        COMM(d.red_dec_loc, d.red_dec, 2);
     }
     LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d));
     LAUNCH(K_COMMIT, hipLaunchKernelGGL(k_commit, dim3(blocks_for(nv)), dim3(kBlock), 0, s, d));
@@ -581,10 +735,20 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     Dev &d = ctx->d;
     *ctx->h_ctrl = init;
     PLBA_CHECK(hipMemcpyAsync(d.ctrl, ctx->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, ctx->stream));
-    const bool use_graph = !ctx->timing;
+    // the host transport synchronises inside the step: no graph then
+    bool use_graph = !ctx->timing && ctx->comm.kind != plba_ctx::Comm::HOST && !ctx->no_graph;
     if (use_graph) {
         int rc = capture_step(ctx);
-        if (rc) return rc;
+        if (rc && ctx->comm.kind == plba_ctx::Comm::RCCL) {
+            // collectives that refuse stream capture: fall back to direct launches for good
+            (void)hipGetLastError();
+            ctx->no_graph = true;
+            use_graph = false;
+            if (ctx->opts.verbose) fprintf(stderr, "[plba] step capture with RCCL failed (%s); direct launches\n",
+                                           ctx->err.c_str());
+        } else if (rc) {
+            return rc;
+        }
     }
     int launched = 0;
     int batch = std::max(4, ctx->last_steps);
@@ -652,6 +816,24 @@ int launch_edges(plba_ctx *ctx, void (*k)(Dev, int), int arg) {
     return PLBA_OK;
 }
 
+// Sharded windows: whole-window landmark states and per-edge outputs on every rank
+// (one all-reduce of a zero-filled, scattered buffer). Collective: all ranks call it.
+int gather_outputs(plba_ctx *ctx, std::vector<double> &out) {
+    Dev &d = ctx->d;
+    const size_t n = (size_t)d.n_lm_g * 4 + 3 * (size_t)d.E_g;
+    PLBA_CHECK(hipMemsetAsync(d.gat, 0, n * sizeof(double), ctx->stream));
+    if (d.Ep) hipLaunchKernelGGL(k_depth, dim3(blocks_for(d.Ep)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth);
+    const int m = std::max(d.n_lm, d.E);
+    if (m) hipLaunchKernelGGL(k_gather, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth);
+    PLBA_CHECK(hipGetLastError());
+    int rc = allreduce(ctx, d.gat, d.gat, n);
+    if (rc) return rc;
+    out.resize(n);
+    PLBA_CHECK(hipMemcpyAsync(out.data(), d.gat, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    return PLBA_OK;
+}
+
 }  // namespace
 
 // ==================================================================================== C ABI
@@ -697,6 +879,8 @@ int plba_destroy(plba_ctx *ctx) {
     ctx->free_all();
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
+    if (ctx->comm.hbuf) (void)hipHostFree(ctx->comm.hbuf);
+    if (ctx->comm.nccl) (void)ncclCommDestroy(ctx->comm.nccl);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return PLBA_OK;
@@ -735,7 +919,7 @@ int plba_set_edge_levels(plba_ctx *ctx, const uint8_t *ept_level, const uint8_t 
     std::vector<uint8_t> lv(E, 0);
     for (int e = 0; e < E; ++e) {
         int o = ctx->e_orig[e];
-        bool is_pt = e < ctx->Ep;
+        bool is_pt = e < ctx->d.Ep;
         lv[e] = is_pt ? (ept_level ? ept_level[o] : 0) : (eln_level ? eln_level[o] : 0);
     }
     ctx->h_level = lv;
@@ -776,6 +960,18 @@ int plba_get_edge_chi2(plba_ctx *ctx, double *ept_chi2, uint8_t *ept_depth_ok, d
     if (!ctx) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
     Dev &d = ctx->d;
+    if (d.sharded) {
+        std::vector<double> gv;
+        int rc = gather_outputs(ctx, gv);
+        if (rc) return rc;
+        const double *o = gv.data() + (size_t)d.n_lm_g * 4;
+        for (int e = 0; e < ctx->Ep; ++e) {
+            if (ept_chi2) ept_chi2[e] = o[e];
+            if (ept_depth_ok) ept_depth_ok[e] = (uint8_t)o[(size_t)d.E_g + e];
+        }
+        for (int e = 0; e < ctx->El && eln_chi2; ++e) eln_chi2[e] = o[ctx->Ep + e];
+        return PLBA_OK;
+    }
     std::vector<double> chi(d.E);
     std::vector<uint8_t> dep(d.Ep);
     if (ept_depth_ok && d.Ep) {
@@ -801,6 +997,18 @@ int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth
     if (!ctx) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
     Dev &d = ctx->d;
+    if (d.sharded) {  // poses are replicated; landmarks come from the gather
+        std::vector<double> gv;
+        int rc = gather_outputs(ctx, gv);
+        if (rc) return rc;
+        if (kf_Tcw && d.n_kf)
+            PLBA_CHECK(hipMemcpy(kf_Tcw, d.T_cur, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
+        for (int p = 0; p < ctx->n_pt && pt_xyz; ++p)
+            for (int k = 0; k < 3; ++k) pt_xyz[3 * p + k] = gv[(size_t)p * 4 + k];
+        for (int l = 0; l < ctx->n_ln && ln_orth; ++l)
+            for (int k = 0; k < 4; ++k) ln_orth[4 * l + k] = gv[(size_t)(ctx->n_pt + l) * 4 + k];
+        return PLBA_OK;
+    }
     std::vector<double> X((size_t)d.n_lm * 4);
     if (kf_Tcw && d.n_kf)
         PLBA_CHECK(hipMemcpyAsync(kf_Tcw, d.T_cur, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost, ctx->stream));
@@ -850,6 +1058,28 @@ int plba_lba_plucker(plba_ctx *ctx, plba_result *res) {
         res->chi2[0] = ctx->h_ctrl->chi2_final[0];
         res->chi2[1] = ctx->h_ctrl->chi2_final[1];
         res->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (d.sharded) {  // one gather for every output
+            std::vector<double> gv;
+            if ((rc = gather_outputs(ctx, gv))) return rc;
+            if (res->kf_Tcw && d.n_kf)
+                PLBA_CHECK(hipMemcpy(res->kf_Tcw, d.T_cur, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
+            for (int p = 0; p < ctx->n_pt && res->pt_xyz; ++p)
+                for (int k = 0; k < 3; ++k) res->pt_xyz[3 * p + k] = gv[(size_t)p * 4 + k];
+            for (int l = 0; l < ctx->n_ln && res->ln_orth; ++l)
+                for (int k = 0; k < 4; ++k) res->ln_orth[4 * l + k] = gv[(size_t)(ctx->n_pt + l) * 4 + k];
+            const double *o = gv.data() + (size_t)d.n_lm_g * 4;
+            const size_t Eg = d.E_g;
+            for (int e = 0; e < ctx->Ep; ++e) {
+                if (res->ept_chi2) res->ept_chi2[e] = o[e];
+                if (res->ept_depth_ok) res->ept_depth_ok[e] = (uint8_t)o[Eg + e];
+                if (res->ept_level) res->ept_level[e] = (uint8_t)o[2 * Eg + e];
+            }
+            for (int e = 0; e < ctx->El; ++e) {
+                if (res->eln_chi2) res->eln_chi2[e] = o[ctx->Ep + e];
+                if (res->eln_level) res->eln_level[e] = (uint8_t)o[2 * Eg + ctx->Ep + e];
+            }
+            return PLBA_OK;
+        }
         if ((rc = plba_download(ctx, res->kf_Tcw, res->pt_xyz, res->ln_orth))) return rc;
         if (res->ept_chi2 || res->ept_depth_ok || res->eln_chi2)
             if ((rc = plba_get_edge_chi2(ctx, res->ept_chi2, res->ept_depth_ok, res->eln_chi2))) return rc;
@@ -906,9 +1136,63 @@ int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [16][8] */) {
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[10] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
-                           ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep};
-    for (int i = 0; i < cap && i < 10; ++i) out[i] = v[i];
+    const int64_t v[12] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+                           ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
+                           ctx->step_exec != nullptr, ctx->d.sharded};
+    for (int i = 0; i < cap && i < 12; ++i) out[i] = v[i];
+    return PLBA_OK;
+}
+
+int plba_shard_plan(const plba_graph *g, int32_t nranks, int32_t *pt_owner, int32_t *ln_owner) {
+    if (!g || nranks < 1 || (g->n_pt && !pt_owner) || (g->n_ln && !ln_owner)) return PLBA_E_INVALID;
+    if ((g->n_ept && (!g->ept_lm || !g->ept_kf)) || (g->n_eln && (!g->eln_lm || !g->eln_kf)) ||
+        (g->n_kf && !g->kf_id))
+        return PLBA_E_INVALID;
+    for (int e = 0; e < g->n_ept; ++e)
+        if (g->ept_lm[e] < 0 || g->ept_lm[e] >= g->n_pt || g->ept_kf[e] < 0 || g->ept_kf[e] >= g->n_kf)
+            return PLBA_E_INVALID;
+    for (int e = 0; e < g->n_eln; ++e)
+        if (g->eln_lm[e] < 0 || g->eln_lm[e] >= g->n_ln || g->eln_kf[e] < 0 || g->eln_kf[e] >= g->n_kf)
+            return PLBA_E_INVALID;
+    shard_plan(g, nranks, pt_owner, ln_owner);
+    return PLBA_OK;
+}
+
+int plba_comm_unique_id(uint8_t id[128]) {
+    if (!id) return PLBA_E_INVALID;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return PLBA_E_COMM;
+    std::memcpy(id, &u, sizeof(u));
+    return PLBA_OK;
+}
+
+int plba_comm_init_rccl(plba_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return PLBA_E_INVALID;
+    if (ctx->comm.kind != plba_ctx::Comm::NONE || ctx->uploaded) return PLBA_E_STATE;
+    (void)hipSetDevice(ctx->opts.device);
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    const ncclResult_t r = ncclCommInitRank(&ctx->comm.nccl, nranks, u, rank);
+    if (r != ncclSuccess) {
+        ctx->set_error("ncclCommInitRank(%d ranks, rank %d): %s", nranks, rank, ncclGetErrorString(r));
+        ctx->comm.nccl = nullptr;
+        return PLBA_E_COMM;
+    }
+    ctx->comm.kind = plba_ctx::Comm::RCCL;
+    ctx->comm.nranks = nranks;
+    ctx->comm.rank = rank;
+    return PLBA_OK;
+}
+
+int plba_comm_init_host(plba_ctx *ctx, int32_t nranks, int32_t rank, plba_host_allreduce_fn fn, void *user) {
+    if (!ctx || !fn || nranks < 1 || rank < 0 || rank >= nranks) return PLBA_E_INVALID;
+    if (ctx->comm.kind != plba_ctx::Comm::NONE || ctx->uploaded) return PLBA_E_STATE;
+    ctx->comm.kind = plba_ctx::Comm::HOST;
+    ctx->comm.nranks = nranks;
+    ctx->comm.rank = rank;
+    ctx->comm.fn = fn;
+    ctx->comm.user = user;
     return PLBA_OK;
 }
 

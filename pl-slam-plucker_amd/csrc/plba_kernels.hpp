@@ -112,6 +112,17 @@ struct Dev {
     double *part_ps;                    // [n_kf_blocks]
     Ctrl *ctrl;
     plba_iter_trace *trace;             // [kTraceCap] per-iteration records written by k_decide
+    // sharded windows: the arrays the ranks sum with one all-reduce each
+    int32_t sharded, nranks, rank;
+    int32_t n_lm_g, E_g;                // whole-window landmark / edge counts
+    // Out-of-place (send *_loc -> receive) so that replaying a step whose kernels were guarded
+    // off re-reduces unchanged partials and leaves the totals intact.
+    double *red_iter, *red_iter_loc;    // [nf*42 + 2 + nranks]: Hpp | b_p | χ² | active | lm max per rank
+    double *red_rcs, *red_rcs_loc;      // [nblk*36 + nf*6]: Σ A₁ᵀZ₁Z₂ᵀA₂ per block | Σ A_eᵀq_e per pose
+    double *red_dec, *red_dec_loc;      // [2]: trial χ² | landmark part of Σx(λx+b)
+    double *Hpp_w, *bp_w;               // where k_pose_reduce writes (== Hpp, bp unless sharded)
+    int32_t *lm_gpos, *e_gpos;          // local landmark / edge -> whole-window position
+    double *gat;                        // [n_lm_g*4 + 3*E_g] final gather buffer
 };
 
 // ---------------------------------------------------------------- block reductions
@@ -275,7 +286,7 @@ __global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
             out[k] = v;
         }
     if (threadIdx.x == 0) {
-        double *H = d.Hpp + (size_t)h * 36;
+        double *H = d.Hpp_w + (size_t)h * 36;
         int idx = 0;
         double mx = 0.0;
         for (int r = 0; r < 6; ++r)
@@ -285,7 +296,7 @@ __global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
                 if (r == cc) mx = fmax(mx, fabs(out[idx]));
                 ++idx;
             }
-        for (int r = 0; r < 6; ++r) d.bp[(size_t)h * 6 + r] = out[21 + r];
+        for (int r = 0; r < 6; ++r) d.bp_w[(size_t)h * 6 + r] = out[21 + r];
         d.part_max[h] = mx;
     }
 }
@@ -327,17 +338,59 @@ __global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
     if (threadIdx.x == 0) d.part_max[d.nf + blockIdx.x] = m;
 }
 
-__global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
+// sharded windows: this rank's χ² and landmark max|diag| into the all-reduced iteration array
+// (Hpp and b_p already sit in it). The rank's max goes to its own slot: the sum over ranks of
+// one-hot slots is the list of maxima, reduced with max by k_iter_init.
+__global__ __launch_bounds__(kBlock) void k_iter_pack(Dev d) {
     ITER_GUARD
     __shared__ double sh[kBlock / 64];
     double s = 0.0;
     for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) s += d.part_chi2[i];
-    double chi = block_sum<kBlock>(s, sh);
+    const double chi = block_sum<kBlock>(s, sh);
     double m = 0.0;
-    for (int i = threadIdx.x; i < d.nf + d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[i]);
-    double mx = block_max<kBlock>(m, sh);
+    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[d.nf + i]);
+    const double mx = block_max<kBlock>(m, sh);
+    double *o = d.red_iter_loc + (size_t)d.nf * 42;
+    if (threadIdx.x == 0) {
+        o[0] = chi;
+        o[1] = d.ctrl->any_active ? 1.0 : 0.0;
+    }
+    for (int r = threadIdx.x; r < d.nranks; r += kBlock) o[2 + r] = r == d.rank ? mx : 0.0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
+    ITER_GUARD
+    __shared__ double sh[kBlock / 64];
+    double chi, mx;
+    bool none_active = false;
+    if (d.sharded) {  // totals from the all-reduced iteration array
+        const double *o = d.red_iter + (size_t)d.nf * 42;
+        double m = 0.0;
+        for (int i = threadIdx.x; i < d.nf * 6; i += kBlock) m = fmax(m, fabs(d.Hpp[(i / 6) * 36 + (i % 6) * 7]));
+        for (int r = threadIdx.x; r < d.nranks; r += kBlock) m = fmax(m, o[2 + r]);
+        mx = block_max<kBlock>(m, sh);
+        chi = o[0];
+        none_active = o[1] == 0.0;
+    } else {
+        double s = 0.0;
+        for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) s += d.part_chi2[i];
+        chi = block_sum<kBlock>(s, sh);
+        double m = 0.0;
+        for (int i = threadIdx.x; i < d.nf + d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[i]);
+        mx = block_max<kBlock>(m, sh);
+    }
     if (threadIdx.x == 0) {
         Ctrl *c = d.ctrl;
+        if (d.sharded && c->iter == 0 && none_active) {
+            // no rank has an active edge: optimize() returns -1 without iterating (the
+            // single-GPU path decides this in k_switch_finish)
+            c->iters_done[c->stage] = -1;
+            c->chi2_final[c->stage] = 0.0;
+            c->need_iter = 0;
+            if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
+            else c->all_done = 1;
+            return;
+        }
         c->currentChi = chi;
         c->chi2_start = chi;
         if (c->iter == 0) {  // computeLambdaInit: τ·max|H_jj|, ν = 2
@@ -415,6 +468,20 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
     }
 }
 
+// sharded pass 2a: this rank's per-block sums (chunks in order) into the all-reduced array
+__global__ __launch_bounds__(kBlock) void k_rcs_blockpart(Dev d) {
+    TRIAL_GUARD
+    const int gid = blockIdx.x * kBlock + threadIdx.x;
+    const int b = gid / 42, e = gid % 42;
+    if (b >= d.nblk) return;
+    const int i1 = d.blk_i1[b];
+    if (e >= 36 && i1 != d.blk_i2[b]) return;
+    double sacc = 0.0;
+    for (int c = d.blk_ch[b]; c < d.blk_ch[b + 1]; ++c) sacc += d.ch_part[(size_t)c * 42 + e];
+    if (e < 36) d.red_rcs_loc[(size_t)b * 36 + e] = sacc;
+    else d.red_rcs_loc[(size_t)d.nblk * 36 + 6 * i1 + (e - 36)] = sacc;
+}
+
 // pass 2: per block entry, sum its chunks in order, add Hpp + λI (diagonal), write the band /
 // dense matrix and b_s = b_p - Σ A_eᵀ q_e.
 __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
@@ -426,7 +493,9 @@ __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
     const bool diag = i1 == i2;
     if (e >= 36 && !diag) return;
     double sacc = 0.0;
-    for (int c = d.blk_ch[b]; c < d.blk_ch[b + 1]; ++c) sacc += d.ch_part[(size_t)c * 42 + e];
+    if (d.sharded) sacc = e < 36 ? d.red_rcs[(size_t)b * 36 + e] : d.red_rcs[(size_t)d.nblk * 36 + 6 * i1 + (e - 36)];
+    else
+        for (int c = d.blk_ch[b]; c < d.blk_ch[b + 1]; ++c) sacc += d.ch_part[(size_t)c * 42 + e];
     const int n = d.n;
     if (e >= 36) {
         d.bs[6 * i1 + (e - 36)] = d.bp[(size_t)i1 * 6 + (e - 36)] - sacc;
@@ -917,7 +986,9 @@ __global__ __launch_bounds__(kBlock) void k_pose_update(Dev d) {
         const double *Tc = d.T_cur + (size_t)k * 12;
         double *Tt = d.T_trial + (size_t)k * 12;
         const int h = d.kf_hidx[k];
-        if (h >= 0 && d.kf_active[k]) {
+        // sharded: a pose's activity is global (another rank may hold its edges); a free pose
+        // with no active edge anywhere has a zero RCS row, x = 0 and an exact identity oplus
+        if (h >= 0 && (d.sharded || d.kf_active[k])) {
             const double lam = d.ctrl->lambda;
             double x[6];
 #pragma unroll
@@ -1141,16 +1212,37 @@ __global__ __launch_bounds__(kBlock) void k_edge_eval(Dev d) {
     if (threadIdx.x == 0) d.part_lm[blockIdx.x] = s1;
 }
 
-// OptimizationAlgorithmLevenberg trial decision (SURVEY.md §8a A13) + optimize() loop control.
-__global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
+// sharded: this rank's trial χ² and landmark scale terms into the all-reduced decision array
+__global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
     TRIAL_GUARD
     __shared__ double sh[kBlock / 64];
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
     for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) b += d.part_lms[i];
-    for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];
-    const double tempChi0 = block_sum<kBlock>(a, sh);
-    const double scale0 = block_sum<kBlock>(b, sh);
+    const double ta = block_sum<kBlock>(a, sh);
+    const double tb = block_sum<kBlock>(b, sh);
+    if (threadIdx.x == 0) {
+        d.red_dec_loc[0] = ta;
+        d.red_dec_loc[1] = tb;
+    }
+}
+
+// OptimizationAlgorithmLevenberg trial decision (SURVEY.md §8a A13) + optimize() loop control.
+__global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
+    TRIAL_GUARD
+    __shared__ double sh[kBlock / 64];
+    double a = 0.0, b = 0.0;
+    if (!d.sharded) {
+        for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
+        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) b += d.part_lms[i];
+    }
+    for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];  // poses: replicated
+    double tempChi0 = block_sum<kBlock>(a, sh);
+    double scale0 = block_sum<kBlock>(b, sh);
+    if (d.sharded) {  // landmark terms summed over ranks
+        tempChi0 = d.red_dec[0];
+        scale0 += d.red_dec[1];
+    }
     if (threadIdx.x != 0) return;
     Ctrl *c = d.ctrl;
     c->steps += 1;
@@ -1199,7 +1291,7 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
 __global__ __launch_bounds__(kBlock) void k_commit(Dev d) {
     if (!d.ctrl->commit_pending) return;
     const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < d.n_kf && d.kf_hidx[i] >= 0 && d.kf_active[i]) {
+    if (i < d.n_kf && d.kf_hidx[i] >= 0 && (d.sharded || d.kf_active[i])) {
 #pragma unroll
         for (int k = 0; k < 12; ++k) d.T_cur[(size_t)i * 12 + k] = d.T_trial[(size_t)i * 12 + k];
     }
@@ -1258,7 +1350,7 @@ __global__ void k_switch_finish(Dev d) {
     c->iter = 0;
     c->robust = c->stage_robust[c->stage];
     c->level = c->stage_level[c->stage];
-    if (!c->any_active) {  // _ivMap empty: optimize() returns -1 without iterating
+    if (!c->any_active && !d.sharded) {  // _ivMap empty: optimize() returns -1 without iterating
         c->iters_done[c->stage] = -1;
         c->chi2_final[c->stage] = 0.0;
         if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
@@ -1295,6 +1387,22 @@ __global__ void k_depth(Dev d, uint8_t *out) {
     double Pc[3];
     point_pc(d.T_cur + (size_t)d.e_kf[e] * 12, d.X_cur + (size_t)d.e_lm[e] * 4, Pc);
     out[e] = Pc[2] > 0.0 ? 1 : 0;
+}
+
+// sharded: scatter this rank's landmark states and per-edge outputs to their whole-window
+// positions (the buffer is zeroed first and summed over ranks afterwards)
+__global__ void k_gather(Dev d, const uint8_t *depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d.n_lm)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d.gat[(size_t)d.lm_gpos[i] * 4 + k] = d.X_cur[(size_t)i * 4 + k];
+    if (i < d.E) {
+        double *o = d.gat + (size_t)d.n_lm_g * 4;
+        const int g = d.e_gpos[i];
+        o[g] = d.chi2_last[i];
+        o[(size_t)d.E_g + g] = i < d.Ep ? (double)depth[i] : 0.0;
+        o[2 * (size_t)d.E_g + g] = (double)d.e_level[i];
+    }
 }
 
 }  // namespace plba

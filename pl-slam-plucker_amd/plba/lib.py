@@ -26,7 +26,11 @@ EXPORTED = [
     "plba_set_edge_levels", "plba_set_robust", "plba_initialize_optimization", "plba_optimize",
     "plba_refresh_edge_errors", "plba_get_edge_chi2", "plba_download", "plba_lba_plucker", "plba_get_trace",
     "plba_synchronize", "plba_enable_kernel_timing", "plba_kernel_times", "plba_structure_stats",
+    "plba_shard_plan", "plba_comm_unique_id", "plba_comm_init_rccl", "plba_comm_init_host",
 ]
+
+# int (*plba_host_allreduce_fn)(void *user, double *buf, int64_t n)
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64)
 
 
 class PlbaError(RuntimeError):
@@ -68,6 +72,10 @@ def load(path: Optional[str] = None):
     L.plba_enable_kernel_timing.argtypes = [vp, C.c_int32]
     L.plba_kernel_times.argtypes = [vp, C.POINTER(C.c_char_p), dp, ip, C.c_int32, ip]
     L.plba_structure_stats.argtypes = [vp, C.POINTER(C.c_int64), C.c_int32]
+    L.plba_shard_plan.argtypes = [C.POINTER(capi.PlbaGraph), C.c_int32, ip, ip]
+    L.plba_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+    L.plba_comm_init_rccl.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
+    L.plba_comm_init_host.argtypes = [vp, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, vp]
     for name in EXPORTED:
         f = getattr(L, name)
         if name not in ("plba_default_opts", "plba_last_error"):
@@ -78,6 +86,27 @@ def load(path: Optional[str] = None):
 
 def _p(a, t=C.c_double):
     return a.ctypes.data_as(C.POINTER(t))
+
+
+def shard_plan(g: Graph, nranks: int):
+    """Landmark -> rank assignment of a sharded window (pure host code; no GPU needed)."""
+    L = load()
+    gv = capi.GraphView(g)
+    po = np.zeros(max(g.n_pt, 1), np.int32)
+    lo = np.zeros(max(g.n_ln, 1), np.int32)
+    rc = L.plba_shard_plan(C.byref(gv.struct), nranks, _p(po, C.c_int32), _p(lo, C.c_int32))
+    if rc != 0:
+        raise PlbaError(f"plba_shard_plan failed: {PLBA_ERRORS.get(rc, rc)}")
+    return po[:g.n_pt], lo[:g.n_ln]
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (create on rank 0, broadcast the 128 bytes)."""
+    buf = (C.c_uint8 * 128)()
+    rc = load().plba_comm_unique_id(buf)
+    if rc != 0:
+        raise PlbaError(f"plba_comm_unique_id failed: {PLBA_ERRORS.get(rc, rc)}")
+    return bytes(buf)
 
 
 class Solver:
@@ -120,6 +149,24 @@ class Solver:
 
     def __exit__(self, *a):
         self.close()
+
+    # -- sharded windows (call one of these before upload)
+    def comm_init_rccl(self, nranks: int, rank: int, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.L.plba_comm_init_rccl(self.ctx, nranks, rank, buf), "plba_comm_init_rccl")
+
+    def comm_init_host(self, nranks: int, rank: int, allreduce):
+        """allreduce(np.ndarray[float64]) sums the array over ranks in place."""
+        def tramp(user, buf, n):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(n,)))
+                return 0
+            except Exception:  # never unwind through C
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._host_cb = HOST_ALLREDUCE_FN(tramp)
+        self._check(self.L.plba_comm_init_host(self.ctx, nranks, rank, self._host_cb, None), "plba_comm_init_host")
 
     # -- g2o-style calls
     def upload(self, g: Graph):
@@ -195,10 +242,10 @@ class Solver:
         return {names[i].decode(): (float(ms[i]), int(nl[i])) for i in range(n.value)}
 
     def structure_stats(self) -> dict:
-        st = (C.c_int64 * 10)()
-        self._check(self.L.plba_structure_stats(self.ctx, st, 10), "plba_structure_stats")
+        st = (C.c_int64 * 12)()
+        self._check(self.L.plba_structure_stats(self.ctx, st, 12), "plba_structure_stats")
         return dict(nf=st[0], bw=st[1], nblk=st[2], triples=st[3], edges=st[4], landmarks=st[5], banded=st[6],
-                    chunks=st[7], free_edges=st[8], point_edges=st[9])
+                    chunks=st[7], free_edges=st[8], point_edges=st[9], graph=st[10], sharded=st[11])
 
     def synchronize(self):
         self._check(self.L.plba_synchronize(self.ctx), "plba_synchronize")

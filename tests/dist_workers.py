@@ -1,0 +1,103 @@
+"""Worker functions for multi-process tests (imported by spawned ranks)."""
+import os
+import socket
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "pl-slam-plucker_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def init_gloo(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def dense_schur_part(g, owned_pt, owned_ln, lam=1e-3):
+    """Reduced camera system contribution of the given landmarks (numpy, oracle Jacobians):
+    Σ_edges JpᵀΩJp − Σ_l Hpl_l (Hll_l+λI)⁻¹ Hpl_lᵀ, and the matching right-hand side."""
+    import oracle_api as oa
+    cam = (g.fx, g.fy, g.cx, g.cy)
+    free = np.nonzero(g.kf_fixed == 0)[0]
+    hid = -np.ones(g.n_kf, int)
+    hid[free[np.argsort(g.kf_id[free], kind="stable")]] = np.arange(len(free))
+    n = 6 * len(free)
+    S, bs = np.zeros((n, n)), np.zeros(n)
+    for kind, owned in (("pt", owned_pt), ("ln", owned_ln)):
+        lm_arr = g.ept_lm if kind == "pt" else g.eln_lm
+        for l in np.nonzero(owned)[0]:
+            D = 3 if kind == "pt" else 4
+            Hll, bl = lam * np.eye(D), np.zeros(D)
+            rows = []
+            for e in np.nonzero(lm_arr == l)[0]:
+                k = (g.ept_kf if kind == "pt" else g.eln_kf)[e]
+                if kind == "pt":
+                    err, Ji, Jj = oa.point_edge(g.kf_Tcw[k], g.pt_xyz[l], g.ept_obs[e], cam)
+                    w = g.ept_info[e]
+                else:
+                    err, Ji, Jj = oa.line_edge(g.kf_Tcw[k], g.ln_orth[l], g.eln_obs[e], cam)
+                    err, Ji, Jj, w = err[:2], Ji[:2], Jj[:2], g.eln_info[e]
+                Hll += w * Ji.T @ Ji
+                bl -= w * Ji.T @ err
+                h = hid[k]
+                if h >= 0:
+                    S[6 * h:6 * h + 6, 6 * h:6 * h + 6] += w * Jj.T @ Jj
+                    bs[6 * h:6 * h + 6] -= w * Jj.T @ err
+                    rows.append((h, w * Jj.T @ Ji))
+            Hinv = np.linalg.inv(Hll)
+            for h1, P1 in rows:
+                bs[6 * h1:6 * h1 + 6] -= P1 @ Hinv @ bl
+                for h2, P2 in rows:
+                    S[6 * h1:6 * h1 + 6, 6 * h2:6 * h2 + 6] -= P1 @ Hinv @ P2.T
+    return S, bs
+
+
+def plan_and_schur_worker(rank, world, port, outdir):
+    """CPU rank: shard plan, partial RCS of the own landmarks, summed over gloo with the
+    product's host all-reduce hook; writes what it saw for the parent to check."""
+    dist = init_gloo(rank, world, port)
+    from plba import synth
+    from plba.dist import host_allreduce
+    from plba.lib import shard_plan
+    g = synth.generate("C1L", fixed_frac=0.2)
+    po, lo = shard_plan(g, world)
+    S, bs = dense_schur_part(g, po == rank, lo == rank)
+    buf = np.concatenate([S.ravel(), bs])
+    host_allreduce()(buf)
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), po=po, lo=lo, sum=buf)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def sharded_gpu_worker(rank, world, port, outdir, cfg, transport):
+    """GPU rank (all ranks may share one GPU with the host transport): full sharded LBA."""
+    dist = init_gloo(rank, world, port)
+    from plba import synth
+    from plba.dist import sharded_solver
+    g = synth.generate(cfg)
+    s = sharded_solver(device=0, transport=transport)
+    s.upload(g)
+    out = s.lba_plucker()
+    s.reset()
+    out2 = s.lba_plucker()
+    st = s.structure_stats()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"),
+             **{k: v for k, v in out.items() if k not in ("trace", "solve_ms")},
+             trace_chi2=np.array([t["chi2_end"] for t in out["trace"]]),
+             rerun_equal=np.array(all(np.array_equal(out[k], out2[k]) for k in ("kf_Tcw", "pt_xyz", "ln_orth"))),
+             local_landmarks=np.array(st["landmarks"]), local_edges=np.array(st["edges"]))
+    s.close()
+    dist.barrier()
+    dist.destroy_process_group()
