@@ -40,14 +40,12 @@ namespace plba {
     } while (0)
 
 enum KernelId {
-    K_SWITCH, K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_SCHUR, K_ESCHUR, K_MEMSET, K_ASSEMBLE,
-    K_FINALIZE, K_FACTOR, K_POSE_UPDATE, K_BACKSUB, K_LM_UPDATE, K_EVAL, K_DECIDE, K_COMMIT, K_COUNT
+    K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_ESCHUR, K_MEMSET, K_ASSEMBLE, K_FINALIZE, K_FACTOR,
+    K_POSE_UPDATE, K_LM_UPDATE, K_EVAL, K_DECIDE, K_COUNT
 };
 static const char *kKernelNames[K_COUNT] = {
-    "k_switch(4)", "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_lm_chol", "k_edge_schur",
-    "memset_rcs",
-    "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_edge_backsub", "k_lm_solve",
-    "k_edge_eval", "k_decide", "k_commit"};
+    "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_edge_schur", "memset_rcs",
+    "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_lm_solve", "k_edge_eval", "k_decide"};
 
 }  // namespace plba
 
@@ -87,6 +85,7 @@ struct plba_ctx {
     hipGraph_t step_graph = nullptr;
     hipGraphExec_t step_exec = nullptr;
     int last_steps = 16;     // steps the previous schedule needed (first batch size)
+    int cur = 0;             // which state buffer holds the current estimate (mirror of Ctrl::cur)
     bool no_graph = false;   // set when the step cannot be captured (RCCL without capture support)
     int steps_launched = 0;
     // kernel timing (optional)
@@ -181,10 +180,7 @@ void shard_plan(const plba_graph *g, int R, int32_t *pt_owner, int32_t *ln_owner
     }
 }
 
-inline size_t band_lds_bytes(int bw) {
-    const size_t W = bw + 1;
-    return sizeof(double) * (W * W * 36 + W * 6 + W * 36 + 72 + W * 6 + W * 6 + 12);
-}
+inline size_t band_lds_bytes(int bw) { return sizeof(double) * band_lds_doubles(bw, 0); }
 template <int... B>
 const void *band_kernel_impl(int bw, std::integer_sequence<int, B...>) {
     const void *k = nullptr;
@@ -194,10 +190,14 @@ const void *band_kernel_impl(int bw, std::integer_sequence<int, B...>) {
 inline const void *band_kernel(int bw) {
     return band_kernel_impl(bw, std::make_integer_sequence<int, kBandMax + 1>{});
 }
-inline void launch_band(Dev &d, size_t lds, hipStream_t s) {
-    const void *k = band_kernel(d.bw);
-    void *args[] = {&d};
-    (void)hipLaunchKernel(k, dim3(1), dim3(kBandNT), args, lds, s);
+template <int... B>
+const void *twisted_kernel_impl(int bw, std::integer_sequence<int, B...>) {
+    const void *k = nullptr;
+    ((bw == B ? (k = (const void *)k_rcs_factor_twisted<B>, 0) : 0), ...);
+    return k;
+}
+inline const void *twisted_kernel(int bw) {
+    return twisted_kernel_impl(bw, std::make_integer_sequence<int, kBandMax + 1>{});
 }
 inline int band_ring(int bw, int nf) {
     const size_t budget = 150 * 1024, base = band_lds_bytes(bw);
@@ -205,9 +205,16 @@ inline int band_ring(int bw, int nf) {
     int R = base + per < budget ? (int)((budget - base - per) / per) : 1;
     return std::max(1, std::min(R, 16));
 }
-inline size_t band_lds_bytes(int bw, int nf) {
-    const int R = band_ring(bw, nf);
-    return band_lds_bytes(bw) + sizeof(double) * ((size_t)R * bw * 36 + (size_t)(R + 1) * (36 + 6));
+inline size_t band_lds_bytes(int bw, int nf) { return sizeof(double) * band_lds_doubles(bw, band_ring(bw, nf)); }
+inline size_t twisted_lds_bytes(int bw, int nf) {
+    return band_lds_bytes(bw, nf) + sizeof(double) * twisted_extra_doubles(bw);
+}
+inline void launch_band(Dev &d, hipStream_t s) {
+    void *args[] = {&d};
+    if (d.twisted)
+        (void)hipLaunchKernel(twisted_kernel(d.bw), dim3(2), dim3(kBandNT), args, twisted_lds_bytes(d.bw, d.nf), s);
+    else
+        (void)hipLaunchKernel(band_kernel(d.bw), dim3(1), dim3(kBandNT), args, band_lds_bytes(d.bw, d.nf), s);
 }
 
 // time a launch when kernel timing is enabled
@@ -486,6 +493,13 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.bw = bw;
     d.band_mode = band_mode ? 1 : 0;
     d.ring = band_ring(bw, nf);
+    // two-sided factorisation when the chain is long enough to halve and the separator's dense
+    // system fits next to the band window in LDS (PLBA_NO_TWIST=1 disables, diagnostics only)
+    const char *no_twist = getenv("PLBA_NO_TWIST");
+    const bool twisted = band_mode && bw >= 1 && nf >= 2 * bw + 16 &&
+                         twisted_lds_bytes(bw, nf) <= 159 * 1024 && !(no_twist && no_twist[0] == '1');
+    d.twisted = twisted ? 1 : 0;
+    d.tw_m = twisted ? (nf - bw) / 2 : 0;
     d.corrected = ctx->opts.corrected_line_jacobian;
     d.cam = Cam{g->fx, g->fy, g->cx, g->cy};
     d.huber_pt = g->huber_pt;
@@ -511,13 +525,12 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     rc = upload_vec(ctx, p, v); \
     if (rc) return rc
     UPLOAD(d.T_init, T);
-    UPLOAD(d.T_cur, T);
-    ALLOC(d.T_trial, T.size());
+    UPLOAD(d.Tb[0], T);
+    ALLOC(d.Tb[1], T.size());
     UPLOAD(d.X_init, X);
-    UPLOAD(d.X_cur, X);
-    ALLOC(d.X_trial, X.size());
+    UPLOAD(d.Xb[0], X);
+    ALLOC(d.Xb[1], X.size());
     UPLOAD(d.kf_hidx, kf_hidx);
-    ALLOC(d.kf_active, n_kf);
     UPLOAD(d.e_lm, e_lm);
     UPLOAD(d.e_kf, e_kf);
     UPLOAD(d.e_hidx, e_hidx);
@@ -546,8 +559,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.bp_w = d.red_iter_loc + (size_t)nf * 36;
     ALLOC(d.Hll, (size_t)n_lm * 10);
     ALLOC(d.bl, (size_t)n_lm * 4);
-    ALLOC(d.Lc, (size_t)n_lm * 10);
-    ALLOC(d.gv, (size_t)n_lm * 4);
     ALLOC(d.Z, (size_t)E * 8);
     ALLOC(d.q, (size_t)E * 2);
     ALLOC(d.xl, (size_t)n_lm * 4);
@@ -566,15 +577,25 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.Lband, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
     ALLOC(d.Kinv, (size_t)nf * 36);
     ALLOC(d.zb, (size_t)nf * 6);
+    if (twisted) {
+        ALLOC(d.Bd2, (size_t)nf * (bw + 1) * 36);
+        ALLOC(d.bs2, (size_t)nf * 6);
+        ALLOC(d.Lband2, (size_t)nf * (bw + 1) * 36);
+        ALLOC(d.Kinv2, (size_t)nf * 36);
+        ALLOC(d.zb2, (size_t)nf * 6);
+        ALLOC(d.tw_sep, 2 * ((size_t)bw * (bw + 1) * 36 + (size_t)bw * 6));
+        ALLOC(d.tw_fail, 2);
+        ALLOC(d.tw_count, 1);
+    }
     ALLOC(d.bs, n);
     ALLOC(d.xp, n);
     ALLOC(d.Wbuf, (size_t)std::max(n, 1) * kTile);
     UPLOAD(d.tile_first, tile_first);
     UPLOAD(d.tile_last, tile_last);
     ALLOC(d.part_chi2, d.n_lin_blocks);
+    ALLOC(d.part_any, d.n_lm_blocks);
     ALLOC(d.part_max, nf + d.n_lm_blocks);
     ALLOC(d.part_lm, std::max(d.n_lin_blocks, d.n_lm_blocks));
-    ALLOC(d.ue, (size_t)E * 4);
     ALLOC(d.Xplk, (size_t)n_lm * 6);
     ALLOC(d.part_lms, d.n_lm_blocks);
     ALLOC(d.part_ps, d.n_kf_blocks);
@@ -593,13 +614,20 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ALLOC(d.gat, (size_t)(n_pt_g + n_ln_g) * 4 + 3 * (size_t)(Ep_g + El_g));
     }
 #ifdef PLBA_STAMPS
-    ALLOC(d.stamps, 16 * 8);
-    PLBA_CHECK(hipMemset(d.stamps, 0, 16 * 8 * sizeof(unsigned long long)));
+    ALLOC(d.stamps, 17 * 8);
+    PLBA_CHECK(hipMemset(d.stamps, 0, 17 * 8 * sizeof(unsigned long long)));
 #endif
 #undef ALLOC
 #undef UPLOAD
     if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)band_lds_bytes(bw, nf)));
+    if (twisted) {
+        PLBA_CHECK(hipFuncSetAttribute(twisted_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)twisted_lds_bytes(bw, nf)));
+        PLBA_CHECK(hipMemset(d.Bd2, 0, sizeof(double) * (size_t)nf * (bw + 1) * 36));
+        PLBA_CHECK(hipMemset(d.tw_count, 0, sizeof(int32_t)));
+        PLBA_CHECK(hipMemset(d.tw_fail, 0, 2 * sizeof(int32_t)));
+    }
     // (zero-sized arrays are allocated with one element: clear exactly what alloc() gave)
     // band blocks outside the envelope (w > i - first_blk[i]) are never assembled and must
     // read as zero: the band kernel sweeps all BW block columns of every row
@@ -612,6 +640,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     PLBA_CHECK(hipDeviceSynchronize());
     ctx->uploaded = true;
     ctx->initialized = false;
+    ctx->cur = 0;
     return PLBA_OK;
 }
 
@@ -660,12 +689,6 @@ int launch_step(plba_ctx *ctx) {
     Dev &d = ctx->d;
     hipStream_t s = ctx->stream;
     const int nv = std::max(std::max(d.n_lm, d.n_kf), 1);
-    LAUNCH(K_SWITCH, {
-        if (d.E > 0) hipLaunchKernelGGL(k_switch_classify, dim3(blocks_for(d.E)), dim3(kBlock), 0, s, d, 5.991);
-        hipLaunchKernelGGL(k_switch_clear, dim3(blocks_for(nv)), dim3(kBlock), 0, s, d);
-        if (d.E > 0) hipLaunchKernelGGL(k_switch_activate, dim3(blocks_for(d.E)), dim3(kBlock), 0, s, d);
-        hipLaunchKernelGGL(k_switch_finish, dim3(1), dim3(64), 0, s, d);
-    });
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
@@ -675,7 +698,6 @@ int launch_step(plba_ctx *ctx) {
     }
     LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) {
-        LAUNCH(K_SCHUR, hipLaunchKernelGGL(k_lm_chol, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
         LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }
     if (d.n > 0) {
@@ -686,12 +708,12 @@ int launch_step(plba_ctx *ctx) {
             COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);
         }
         LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
-        if (d.band_mode) LAUNCH(K_FACTOR, launch_band(d, band_lds_bytes(d.bw, d.nf), s));
+        if (d.band_mode) LAUNCH(K_FACTOR, launch_band(d, s));
         else LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
     }
-    if (d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(d.n_kf_blocks), dim3(kBlock), 0, s, d));
+    // the factorisation kernels end with the pose update; without free poses it runs alone
+    if (d.n == 0 && d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(1), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) {
-        LAUNCH(K_BACKSUB, hipLaunchKernelGGL(k_edge_backsub, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
         LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
         LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }
@@ -700,7 +722,6 @@ int launch_step(plba_ctx *ctx) {
         COMM(d.red_dec_loc, d.red_dec, 2);
     }
     LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d));
-    LAUNCH(K_COMMIT, hipLaunchKernelGGL(k_commit, dim3(blocks_for(nv)), dim3(kBlock), 0, s, d));
     return PLBA_OK;
 }
 
@@ -774,6 +795,7 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     }
     ctx->steps_launched = launched;
     ctx->last_steps = std::max(4, ctx->h_ctrl->steps + 1);
+    ctx->cur = ctx->h_ctrl->cur;
     // per-iteration trace written by k_decide
     const int nt = std::min(ctx->h_ctrl->ntrace, kTraceCap);
     std::vector<plba_iter_trace> tr(nt);
@@ -789,6 +811,7 @@ Ctrl schedule_init(plba_ctx *ctx, int n_stages) {
     c.switch_pending = 1;
     c.solve_ok = 1;
     c.max_trials = ctx->opts.max_trials;
+    c.cur = ctx->cur;
     return c;
 }
 
@@ -899,8 +922,10 @@ int plba_upload(plba_ctx *ctx, const plba_graph *g) {
 int plba_reset_estimates(plba_ctx *ctx) {
     if (!ctx || !ctx->uploaded) return ctx ? PLBA_E_STATE : PLBA_E_INVALID;
     Dev &d = ctx->d;
-    PLBA_CHECK(hipMemcpyAsync(d.T_cur, d.T_init, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToDevice, ctx->stream));
-    PLBA_CHECK(hipMemcpyAsync(d.X_cur, d.X_init, sizeof(double) * (size_t)d.n_lm * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    ctx->cur = 0;
+    PLBA_CHECK(hipMemcpyAsync(d.Tb[0], d.T_init, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToDevice, ctx->stream));
+    PLBA_CHECK(hipMemcpyAsync(d.Xb[0], d.X_init, sizeof(double) * (size_t)d.n_lm * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    PLBA_CHECK(hipMemsetAsync(&d.ctrl->cur, 0, sizeof(int32_t), ctx->stream));
     PLBA_CHECK(hipMemsetAsync(d.e_level, 0, std::max(d.E, 1), ctx->stream));
     PLBA_CHECK(hipMemsetAsync(d.xp, 0, sizeof(double) * std::max(d.n, 1), ctx->stream));
     PLBA_CHECK(hipMemsetAsync(d.xl, 0, sizeof(double) * std::max((size_t)d.n_lm * 4, (size_t)1), ctx->stream));
@@ -1002,7 +1027,7 @@ int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth
         int rc = gather_outputs(ctx, gv);
         if (rc) return rc;
         if (kf_Tcw && d.n_kf)
-            PLBA_CHECK(hipMemcpy(kf_Tcw, d.T_cur, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
+            PLBA_CHECK(hipMemcpy(kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
         for (int p = 0; p < ctx->n_pt && pt_xyz; ++p)
             for (int k = 0; k < 3; ++k) pt_xyz[3 * p + k] = gv[(size_t)p * 4 + k];
         for (int l = 0; l < ctx->n_ln && ln_orth; ++l)
@@ -1011,8 +1036,8 @@ int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth
     }
     std::vector<double> X((size_t)d.n_lm * 4);
     if (kf_Tcw && d.n_kf)
-        PLBA_CHECK(hipMemcpyAsync(kf_Tcw, d.T_cur, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost, ctx->stream));
-    if (d.n_lm) PLBA_CHECK(hipMemcpyAsync(X.data(), d.X_cur, sizeof(double) * X.size(), hipMemcpyDeviceToHost, ctx->stream));
+        PLBA_CHECK(hipMemcpyAsync(kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost, ctx->stream));
+    if (d.n_lm) PLBA_CHECK(hipMemcpyAsync(X.data(), d.Xb[ctx->cur], sizeof(double) * X.size(), hipMemcpyDeviceToHost, ctx->stream));
     PLBA_CHECK(hipStreamSynchronize(ctx->stream));
     if (pt_xyz)
         for (int p = 0; p < d.n_pt; ++p)
@@ -1062,7 +1087,7 @@ int plba_lba_plucker(plba_ctx *ctx, plba_result *res) {
             std::vector<double> gv;
             if ((rc = gather_outputs(ctx, gv))) return rc;
             if (res->kf_Tcw && d.n_kf)
-                PLBA_CHECK(hipMemcpy(res->kf_Tcw, d.T_cur, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
+                PLBA_CHECK(hipMemcpy(res->kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
             for (int p = 0; p < ctx->n_pt && res->pt_xyz; ++p)
                 for (int k = 0; k < 3; ++k) res->pt_xyz[3 * p + k] = gv[(size_t)p * 4 + k];
             for (int l = 0; l < ctx->n_ln && res->ln_orth; ++l)
@@ -1122,10 +1147,10 @@ int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *la
 }
 
 // Diagnostic build only: per-wave, per-phase cycle sums of the banded factorisation.
-int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [16][8] */) {
+int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [17][8] */) {
 #ifdef PLBA_STAMPS
     if (!ctx || !ctx->d.stamps) return PLBA_E_STATE;
-    PLBA_CHECK(hipMemcpy(out, ctx->d.stamps, 16 * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    PLBA_CHECK(hipMemcpy(out, ctx->d.stamps, 17 * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return PLBA_OK;
 #else
     (void)ctx; (void)out;
@@ -1136,10 +1161,10 @@ int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [16][8] */) {
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[12] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+    const int64_t v[13] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
-                           ctx->step_exec != nullptr, ctx->d.sharded};
-    for (int i = 0; i < cap && i < 12; ++i) out[i] = v[i];
+                           ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted};
+    for (int i = 0; i < cap && i < 13; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

@@ -6,21 +6,21 @@
 //   k_pose_reduce      pose-parallel deterministic segmented sum: Hpp, b_p
 //   k_landmark_reduce  landmark-parallel: Hll, b_l; max|diag| partials
 //   k_iter_init        χ²_cur, λ init (τ·max|H_jj|, iteration 0)
-// Stage switch (initializeOptimization): k_switch_classify / _clear / _activate / _finish.
+// Stage switch (initializeOptimization): folded into the iteration kernels of the first step
+// of a stage — k_linearize classifies and activates edges, k_landmark_reduce activates
+// landmarks, k_iter_init advances the stage (or skips it when nothing is active).
 // Per damped trial (TRIAL_GUARD):
-//   k_lm_chol          landmark-parallel: (Hll+λI) = LLᵀ, g = L⁻¹ b_l
-//   k_edge_schur       edge-parallel: Z_e = B_e L⁻ᵀ, q_e = Z_e g
+//   k_edge_schur       edge-parallel: (Hll+λI) = LLᵀ of its landmark, Z_e = B_e L⁻ᵀ, q_e = Z_e L⁻¹b_l
 //   k_rcs_chunk        one wave per chunk of <=128 (e1,e2) triples of one RCS block:
 //                      Σ A₁ᵀ(Z₁Z₂ᵀ)A₂ (and Σ A_eᵀq_e on diagonal blocks)
 //   k_rcs_finalize     per block entry: Hpp+λI − Σ chunks into the band (or dense) matrix, b_s
 //   k_rcs_factor_band<BW>  one workgroup: block-banded LDLᵀ + forward/backward solve
 //                      (LinearSolverEigen); k_rcs_factor is the dense-envelope fallback (bw>20)
-//   k_pose_update      oplus of the free poses, pose part of Σx(λx+b)
-//   k_edge_backsub     edge-parallel: u_e = B_eᵀ A_e x_p
-//   k_lm_solve         landmark-parallel: x_l = L⁻ᵀL⁻¹(b_l − Σu_e), oplus, Σx(λx+b) partials
+//                      ... each ending with the pose oplus of the free poses (pose_update_wg)
+//   k_lm_solve         landmark-parallel: x_l = L⁻ᵀL⁻¹(b_l − Σ_e B_eᵀA_e x_p), oplus, Σx(λx+b) partials
 //   k_edge_eval        edge-parallel: χ² at the trial state, robust partial sums
 //   k_decide           ρ, accept/reject, λ/ν update, optimize() loop control (g2o Levenberg)
-//   k_commit           trial -> current on accept (push/pop/discardTop)
+//                      (accepting flips Ctrl::cur: the trial buffer becomes the current state)
 // After the schedule: k_refresh (level-1 computeError) and k_depth (isDepthPositive).
 // All reductions are fixed-order trees: results are bitwise reproducible run to run.
 #pragma once
@@ -54,7 +54,7 @@ struct Ctrl {
     int32_t all_done, switch_pending, robust, level;
     int32_t max_iters[2], iters_done[2];
     int32_t stage_robust[2], stage_level[2], stage_classify[2];
-    int32_t max_trials, ntrace, any_active, commit_pending;
+    int32_t max_trials, ntrace, any_active, cur;      // cur: which state buffer is current
     int32_t steps;                                     // step graphs that did work (diagnostic)
     int32_t pad[3];
 };
@@ -66,10 +66,11 @@ struct Dev {
     Cam cam;
     double huber_pt, huber_ln, tau;
     // state
-    double *T_cur, *T_trial, *T_init;   // [n_kf][12]
-    double *X_cur, *X_trial, *X_init;   // [n_lm][4]
+    // state buffers: Tb[ctrl->cur] is the current estimate, Tb[cur^1] the trial; accepting a trial
+    // flips ctrl->cur (g2o's push/pop/discardTop without a copy)
+    double *Tb[2], *T_init;             // [n_kf][12]
+    double *Xb[2], *X_init;             // [n_lm][4]
     int32_t *kf_hidx;                   // [n_kf]
-    uint8_t *kf_active;                 // [n_kf]
     // edges, landmark-major CSR order (points first, then lines)
     int32_t *e_lm, *e_kf, *e_hidx;      // [E]
     double *e_obs;                      // [E][4]
@@ -83,7 +84,7 @@ struct Dev {
     double *Hpp, *bp;                   // [nf][36], [nf][6]
     double *Hll, *bl;                   // [n_lm][10], [n_lm][4]
     // Schur
-    double *Lc, *gv, *Z, *q, *xl;       // [n_lm][10], [n_lm][4], [E][8], [E][2], [n_lm][4]
+    double *Z, *q, *xl;                 // [E][8], [E][2], [n_lm][4]
     // reduced camera system
     int32_t *blk_i1, *blk_i2, *blk_off; // [nblk], [nblk], [nblk+1]
     int32_t *trip;                      // [T][2]
@@ -105,9 +106,9 @@ struct Dev {
     double *zb;                         // [nf][6]         z = D_B^{-1} y
     // reductions
     double *part_chi2;                  // [n_lin_blocks]
+    int32_t *part_any;                  // [n_lm_blocks] block has an active landmark
     double *part_max;                   // [nf + n_lm_blocks]
     double *part_lm, *part_lms;         // [n_lin_blocks] trial χ² partials, [n_lm_blocks] scale partials
-    double *ue;                         // [E][4]  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)
     double *Xplk;                       // [n_lm][6] trial Plücker of lines (xyz of points)
     double *part_ps;                    // [n_kf_blocks]
     Ctrl *ctrl;
@@ -123,7 +124,19 @@ struct Dev {
     double *Hpp_w, *bp_w;               // where k_pose_reduce writes (== Hpp, bp unless sharded)
     int32_t *lm_gpos, *e_gpos;          // local landmark / edge -> whole-window position
     double *gat;                        // [n_lm_g*4 + 3*E_g] final gather buffer
+    // two-sided banded factorisation (k_rcs_factor_twisted)
+    int32_t twisted, tw_m;              // enabled; rows 0..tw_m-1 top-down, separator tw_m..tw_m+bw-1
+    double *Bd2, *bs2;                  // block-reversed band / rhs (row r' = nf-1-i)
+    double *Lband2, *Kinv2, *zb2;       // factors of the bottom segment (reversed numbering)
+    double *tw_sep;                     // [2][bw][bw+1][36] + [2][bw][6] separator windows
+    int32_t *tw_fail, *tw_count;        // [2] per-segment failure, arrival counter
 };
+
+
+__device__ __forceinline__ double *Tcur(const Dev &d) { return d.Tb[d.ctrl->cur]; }
+__device__ __forceinline__ double *Ttrial(const Dev &d) { return d.Tb[d.ctrl->cur ^ 1]; }
+__device__ __forceinline__ double *Xcur(const Dev &d) { return d.Xb[d.ctrl->cur]; }
+__device__ __forceinline__ double *Xtrial(const Dev &d) { return d.Xb[d.ctrl->cur ^ 1]; }
 
 // ---------------------------------------------------------------- block reductions
 __device__ __forceinline__ double wave_sum(double v) {
@@ -176,6 +189,14 @@ __device__ __forceinline__ bool is_point_lm(const Dev &d, int lm) { return lm < 
 #define STAMP(slot) do {} while (0)
 #endif
 
+// Wave-level LDS ordering: this wave's LDS writes are complete and visible to its other lanes.
+// Unlike a wavefront fence it does not wait for global loads/stores (vmcnt), so prefetches and
+// result stores stay in flight across it.
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Workgroup barrier that orders LDS only: global stores/prefetch loads stay in flight across it
 // (__syncthreads() would drain vmcnt and put an L2 round trip on every step of a serial chain).
 __device__ __forceinline__ void lds_barrier() {
@@ -183,12 +204,15 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // ---------------------------------------------------------------- linearisation
-#define ITER_GUARD                                   \
-    {                                                \
-        const Ctrl *cg = d.ctrl;                     \
-        if (cg->all_done || !cg->need_iter) return;  \
+// iteration kernels run for a new outer iteration and for the first one of a stage (the stage
+// switch — SparseOptimizer::initializeOptimization — is folded into them)
+#define ITER_GUARD                                                           \
+    {                                                                        \
+        const Ctrl *cg = d.ctrl;                                             \
+        if (cg->all_done || !(cg->need_iter || cg->switch_pending)) return;  \
     }
-// a stage skipped by k_switch_finish (no active edge) leaves switch_pending set: no trial
+constexpr double kChi2Thr = 5.991;  // src/mapHandler.cpp:6129,6142
+// a stage skipped by k_iter_init (no active edge) leaves switch_pending set: no trial
 #define TRIAL_GUARD                                          \
     {                                                        \
         const Ctrl *cg = d.ctrl;                             \
@@ -200,12 +224,30 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
     __shared__ double sh[kBlock / 64];
     const int e = blockIdx.x * kBlock + threadIdx.x;
     double rc = 0.0;
+    const Ctrl *cc = d.ctrl;
+    const bool sw = cc->switch_pending;
+    const int nxt = cc->stage + 1;
+    const int robust = sw ? cc->stage_robust[nxt] : cc->robust;
     if (e < d.E) {
         double *A = d.A + (size_t)e * 12, *c = d.cvec + (size_t)e * 2, *B = d.B + (size_t)e * 8;
+        if (sw) {
+            // stage switch: classify on the stale χ² and the current depth (src/mapHandler.cpp:
+            // 6125-6147), then activate the edges of the optimised level
+            if (cc->stage_classify[nxt]) {
+                bool bad = d.chi2_last[e] > kChi2Thr;
+                if (e < d.Ep) {
+                    double Pc[3];
+                    point_pc(Tcur(d) + (size_t)d.e_kf[e] * 12, Xcur(d) + (size_t)d.e_lm[e] * 4, Pc);
+                    bad = bad || !(Pc[2] > 0.0);
+                }
+                if (bad) d.e_level[e] = 1;
+            }
+            d.e_active[e] = d.e_level[e] == cc->stage_level[nxt] ? 1 : 0;
+        }
         if (d.e_active[e]) {
             const int lm = d.e_lm[e], kf = d.e_kf[e];
-            const double *T = d.T_cur + (size_t)kf * 12;
-            const double *X = d.X_cur + (size_t)lm * 4;
+            const double *T = Tcur(d) + (size_t)kf * 12;
+            const double *X = Xcur(d) + (size_t)lm * 4;
             const double *obs = d.e_obs + (size_t)e * 4;
             double err[2], Jl[8], Jp[12];
             double delta;
@@ -226,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
             const double chi = err[0] * (info * err[0]) + err[1] * (info * err[1]);
             d.chi2_last[e] = chi;
             double rho0 = chi, rho1 = 1.0;
-            if (d.ctrl->robust) huber(chi, delta, rho0, rho1);
+            if (robust) huber(chi, delta, rho0, rho1);
             rc = rho0;
             const double s = sqrt(rho1 * info);
             const bool pose_free = d.e_hidx[e] >= 0;
@@ -308,8 +350,16 @@ __global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
     ITER_GUARD
     __shared__ double sh[kBlock / 64];
     const int l = blockIdx.x * kBlock + threadIdx.x;
+    const bool sw = d.ctrl->switch_pending;
     double mx = 0.0;
+    bool any = false;
     if (l < d.n_lm) {
+        if (sw) {  // a landmark is active iff it has an active edge
+            bool act = false;
+            for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) act = act || d.e_active[e];
+            d.lm_active[l] = act ? 1 : 0;
+        }
+        any = d.lm_active[l] != 0;
         double H[10], b[4];
 #pragma unroll
         for (int k = 0; k < 10; ++k) H[k] = 0.0;
@@ -335,7 +385,11 @@ __global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
         mx = fmax(fmax(fabs(H[pk(0, 0)]), fabs(H[pk(1, 1)])), fmax(fabs(H[pk(2, 2)]), fabs(H[pk(3, 3)])));
     }
     double m = block_max<kBlock>(mx, sh);
-    if (threadIdx.x == 0) d.part_max[d.nf + blockIdx.x] = m;
+    const int anyb = __syncthreads_or(any ? 1 : 0);
+    if (threadIdx.x == 0) {
+        d.part_max[d.nf + blockIdx.x] = m;
+        d.part_any[blockIdx.x] = anyb;
+    }
 }
 
 // sharded windows: this rank's χ² and landmark max|diag| into the all-reduced iteration array
@@ -350,10 +404,13 @@ __global__ __launch_bounds__(kBlock) void k_iter_pack(Dev d) {
     double m = 0.0;
     for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[d.nf + i]);
     const double mx = block_max<kBlock>(m, sh);
+    int any = 0;
+    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) any |= d.part_any[i];
+    any = __syncthreads_or(any);
     double *o = d.red_iter_loc + (size_t)d.nf * 42;
     if (threadIdx.x == 0) {
         o[0] = chi;
-        o[1] = d.ctrl->any_active ? 1.0 : 0.0;
+        o[1] = any ? 1.0 : 0.0;
     }
     for (int r = threadIdx.x; r < d.nranks; r += kBlock) o[2 + r] = r == d.rank ? mx : 0.0;
 }
@@ -362,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
     ITER_GUARD
     __shared__ double sh[kBlock / 64];
     double chi, mx;
-    bool none_active = false;
+    bool any;
     if (d.sharded) {  // totals from the all-reduced iteration array
         const double *o = d.red_iter + (size_t)d.nf * 42;
         double m = 0.0;
@@ -370,7 +427,7 @@ __global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
         for (int r = threadIdx.x; r < d.nranks; r += kBlock) m = fmax(m, o[2 + r]);
         mx = block_max<kBlock>(m, sh);
         chi = o[0];
-        none_active = o[1] == 0.0;
+        any = o[1] != 0.0;
     } else {
         double s = 0.0;
         for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) s += d.part_chi2[i];
@@ -378,18 +435,26 @@ __global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
         double m = 0.0;
         for (int i = threadIdx.x; i < d.nf + d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[i]);
         mx = block_max<kBlock>(m, sh);
+        int a = 0;
+        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) a |= d.part_any[i];
+        any = __syncthreads_or(a) != 0;
     }
     if (threadIdx.x == 0) {
         Ctrl *c = d.ctrl;
-        if (d.sharded && c->iter == 0 && none_active) {
-            // no rank has an active edge: optimize() returns -1 without iterating (the
-            // single-GPU path decides this in k_switch_finish)
-            c->iters_done[c->stage] = -1;
-            c->chi2_final[c->stage] = 0.0;
-            c->need_iter = 0;
-            if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
-            else c->all_done = 1;
-            return;
+        if (c->switch_pending) {  // initializeOptimization(level) of the next stage
+            c->switch_pending = 0;
+            c->stage += 1;
+            c->iter = 0;
+            c->robust = c->stage_robust[c->stage];
+            c->level = c->stage_level[c->stage];
+            if (!any) {  // _ivMap empty: optimize() returns -1 without iterating
+                c->iters_done[c->stage] = -1;
+                c->chi2_final[c->stage] = 0.0;
+                c->need_iter = 0;
+                if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
+                else c->all_done = 1;
+                return;
+            }
         }
         c->currentChi = chi;
         c->chi2_start = chi;
@@ -498,7 +563,9 @@ __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
         for (int c = d.blk_ch[b]; c < d.blk_ch[b + 1]; ++c) sacc += d.ch_part[(size_t)c * 42 + e];
     const int n = d.n;
     if (e >= 36) {
-        d.bs[6 * i1 + (e - 36)] = d.bp[(size_t)i1 * 6 + (e - 36)] - sacc;
+        const double v = d.bp[(size_t)i1 * 6 + (e - 36)] - sacc;
+        d.bs[6 * i1 + (e - 36)] = v;
+        if (d.twisted) d.bs2[6 * (d.nf - 1 - i1) + (e - 36)] = v;
         return;
     }
     const int r = e / 6, c = e % 6;
@@ -507,10 +574,45 @@ __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
         if (r == c) h += d.ctrl->lambda;
         if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
         else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
+        if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1)) * 36 + e] = h;
     } else {
         if (d.band_mode) d.Bd[((size_t)i2 * (d.bw + 1) + (i2 - i1)) * 36 + c * 6 + r] = -sacc;
         else d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -sacc;
+        // reversed row nf-1-i1 holds block (i1, i2) = (i1, i1 + w) in its natural orientation
+        if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1) + (i2 - i1)) * 36 + r * 6 + c] = -sacc;
     }
+}
+
+// oplus of every free pose with x_p (trial state; fixed poses copied), and the pose part of
+// Σx(λx+b), reduced over the NT threads of one workgroup into part_ps[0] (other slots zeroed)
+template <int NT>
+__device__ __forceinline__ void pose_update_wg(const Dev &d) {
+    __shared__ double sh_pu[NT / 64];
+    double sc = 0.0;
+    const double lam = d.ctrl->lambda;
+    const double *Tc0 = Tcur(d);
+    double *Tt0 = Ttrial(d);
+    for (int k = threadIdx.x; k < d.n_kf; k += NT) {
+        const double *Tc = Tc0 + (size_t)k * 12;
+        double *Tt = Tt0 + (size_t)k * 12;
+        const int h = d.kf_hidx[k];
+        // a free pose with no active edge has a zero RCS row: x = 0 exactly and the oplus is an
+        // exact identity, so every free pose is updated
+        if (h >= 0) {
+            double x[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                x[i] = d.xp[6 * h + i];
+                sc += x[i] * (lam * x[i] + d.bp[(size_t)h * 6 + i]);
+            }
+            pose_oplus(Tc, x, Tt);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Tt[i] = Tc[i];
+        }
+    }
+    const double s = block_sum<NT>(sc, sh_pu);
+    for (int i = threadIdx.x; i < d.n_kf_blocks; i += NT) d.part_ps[i] = i == 0 ? s : 0.0;
 }
 
 // Envelope-aware tiled LDLᵀ of the lower triangle + solve, one workgroup of 1024 threads.
@@ -602,7 +704,7 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
     }
     __syncthreads();
     if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
-    if (s_fail) return;  // x_p keeps its previous value (g2o leaves _x untouched on failure)
+    if (!s_fail) {  // on failure x_p keeps its previous value (g2o leaves _x untouched)
     // ---- solve L D Lᵀ x = b_s
     double *y = d.Wbuf;  // reuse: y[0..n)
     for (int i = tid; i < n; i += kFacThreads) y[i] = d.bs[i];
@@ -655,6 +757,9 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
         __syncthreads();
     }
     for (int i = tid; i < n; i += kFacThreads) d.xp[i] = y[i];
+    }
+    __syncthreads();
+    pose_update_wg<kFacThreads>(d);  // the update is applied even after a failed solve (A13)
 }
 
 
@@ -680,7 +785,10 @@ __device__ __forceinline__ double gj_inverse6(double M, int lane, bool &fail) {
     double I = (mat && r == c) ? 1.0 : (rhs ? M : 0.0);  // rhs lanes carry y in I
 #pragma unroll
     for (int p = 0; p < 6; ++p) {
-        const double piv = __shfl(M, 7 * p, 64);
+        // the pivot comes from a compile-time lane: v_readlane (SGPR broadcast) instead of an
+        // LDS-crossbar round trip, so its reciprocal overlaps the three row/column permutes
+        const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(M), 7 * p),
+                                            __builtin_amdgcn_readlane(__double2loint(M), 7 * p));
         const double f = __shfl(M, r * 6 + p, 64);
         double ip = __shfl(I, rhs ? 36 + p : p * 6 + c, 64);
         double mp = __shfl(M, p * 6 + c, 64);
@@ -700,9 +808,44 @@ __device__ __forceinline__ double gj_inverse6(double M, int lane, bool &fail) {
 // while waves 1..15 compute the other L blocks and the trailing updates of step k
 // (2 LDS-only barriers per step). Each worker's entries and LDS offsets are compile-time /
 // hoisted; window slots advance incrementally (no runtime modulo in the loop).
+//
+// band_forward eliminates the first `nsteps` block rows of an `nrows`-row band (forward
+// substitution folded in) and, when `sep` is given, stores the updated rows
+// nsteps..nsteps+BW-1 — the separator a second segment meets (k_rcs_factor_twisted).
+struct BandSeg {
+    const double *Bd, *bs;     // [nrows][BW+1][36] block (i, i-w) row-major, [nrows][6]
+    double *Lband, *Kinv, *zb; // outputs, indexed by this segment's row numbering
+    int nrows, nsteps;
+    double *sep;               // nullable: [BW][BW+1][36] + [BW][6]
+};
+
 template <int BW>
-__global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
-    TRIAL_GUARD
+__device__ __forceinline__ void band_lds(double *lds, int R, double *&win, double *&bwin, double *&Lcol, double *&Kv,
+                                         double *&xr, double *&part, double *&ys, double *&ringL, double *&ringK,
+                                         double *&ringZ) {
+    constexpr int W = BW + 1;
+    win = lds;                            // [W slots][W][36]
+    bwin = win + (size_t)W * W * 36;      // [W][6]
+    Lcol = bwin + (size_t)W * 6;          // [W][36]  (index w = 1..BW)
+    Kv = Lcol + (size_t)W * 36;           // [2][36]  S_k^{-1} double buffer
+    xr = Kv + 72;                         // [W][6]  ring of solved x blocks
+    part = xr + (size_t)W * 6;            // [W][6]
+    ys = part + (size_t)W * 6;            // [2][6]  y_k snapshots
+    ringL = ys + 12;                      // [R][BW][36]
+    ringK = ringL + (size_t)R * BW * 36;  // [R+1][36]
+    ringZ = ringK + (size_t)(R + 1) * 36; // [R+1][6]
+}
+// doubles of the band layout above, and of the twisted kernel's extra regions behind it
+__host__ __device__ constexpr size_t band_lds_doubles(int bw, int R) {
+    return (size_t)(bw + 1) * (bw + 1) * 36 + (size_t)(bw + 1) * (6 + 36 + 6 + 6) + 72 + 12 + (size_t)R * bw * 36 +
+           (size_t)(R + 1) * 42;
+}
+__host__ __device__ constexpr size_t twisted_extra_doubles(int bw) {
+    return 2 * (size_t)(bw + 1) * 6 + (size_t)(6 * bw) * (6 * bw + 1) + 72 * (size_t)bw;
+}
+
+template <int BW>
+__device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int ring, unsigned long long *stamps) {
     constexpr int NT = kBandNT, W = BW + 1, NW = NT - 64;
     constexpr int NPAIR = BW * (BW + 1) / 2;             // trailing (wi >= wj >= 1) block pairs
     constexpr int PPT0 = (NPAIR * 36 - 36 + NW - 1) / NW; // pair entries per worker (pair 0 = wave 0)
@@ -710,20 +853,11 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
     constexpr int LPT = ((BW > 1 ? BW - 1 : 0) * 36 + NW - 1) / NW;  // L entries per worker (w >= 2)
     constexpr int RFT = (W * 36 + NW - 1) / NW;           // refill entries per worker
     constexpr int NPT = (NPAIR * 36 > 36) ? NPAIR * 36 : 36; // valid pair-entry bound
-    extern __shared__ double lds[];
-    const int nf = d.nf;
-    double *win = lds;                            // [W slots][W][36]
-    double *bwin = win + (size_t)W * W * 36;      // [W][6]
-    double *Lcol = bwin + (size_t)W * 6;          // [W][36]  (index w = 1..BW)
-    double *Kv = Lcol + (size_t)W * 36;           // [2][36]  S_k^{-1} double buffer
-    double *xr = Kv + 72;                         // [W][6]  ring of solved x blocks
-    double *part = xr + (size_t)W * 6;            // [W][6]
-    double *ys = part + (size_t)W * 6;            // [2][6]  y_k snapshots
-    const int R = d.ring;
+    const int nrows = g.nrows, nsteps = g.nsteps;
+    double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
+    band_lds<BW>(lds, ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
+    const int R = ring;
     const int RK = R + 1;                         // S^-1 / z of step k+1 are written during step k
-    double *ringL = ys + 12;                      // [R][BW][36]
-    double *ringK = ringL + (size_t)R * BW * 36;  // [RK][36]
-    double *ringZ = ringK + (size_t)RK * 36;      // [RK][6]
     __shared__ int s_fail;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -732,9 +866,9 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
     if (tid == 0) s_fail = 0;
     for (int t = tid; t < W * W * 36; t += NT) {
         const int row = t / (W * 36), rem = t % (W * 36);
-        win[t] = (row < nf) ? d.Bd[((size_t)row * W) * 36 + rem] : 0.0;
+        win[t] = (row < nrows) ? g.Bd[((size_t)row * W) * 36 + rem] : 0.0;
     }
-    for (int t = tid; t < W * 6; t += NT) bwin[t] = (t / 6 < nf) ? d.bs[t] : 0.0;
+    for (int t = tid; t < W * 6; t += NT) bwin[t] = (t / 6 < nrows) ? g.bs[t] : 0.0;
     // ---- per-worker static assignment
     int p_wi[PPT], p_wj[PPT], p_li[PPT], p_aj[PPT], p_dst[PPT];
 #pragma unroll
@@ -760,10 +894,10 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
     double pf[RFT], pfn[RFT];
     double pfb = 0.0, pfbn = 0.0;
     auto prefetch = [&](int row, double (&dst)[RFT], double &dstb) {
-        const int rr = min(row, nf - 1);
+        const int rr = min(row, nrows - 1);
 #pragma unroll
-        for (int q = 0; q < RFT; ++q) dst[q] = d.Bd[((size_t)rr * W) * 36 + min(max(wt, 0) + q * NW, W * 36 - 1)];
-        dstb = d.bs[(size_t)rr * 6 + min(max(wt, 0), 5)];
+        for (int q = 0; q < RFT; ++q) dst[q] = g.Bd[((size_t)rr * W) * 36 + min(max(wt, 0) + q * NW, W * 36 - 1)];
+        dstb = g.bs[(size_t)rr * 6 + min(max(wt, 0), 5)];
     };
     if (!crit) prefetch(W, pfn, pfbn);
     __syncthreads();
@@ -786,10 +920,10 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
     int sk = 0, kR = 0, kRK = 1;                  // k % W, k % R, (k+1) % RK
-    for (int k = 0; k < nf; ++k) {
+    for (int k = 0; k < nsteps; ++k) {
         if (s_fail) break;
         const int kb = k & 1;
-        const int wmax = min(BW, nf - 1 - k);
+        const int wmax = min(BW, nrows - 1 - k);
         const double *Kk = Kv + kb * 36;
         const double *yk = ys + kb * 6;
         auto slot = [&](int w) { const int x = sk + w; return x >= W ? x - W : x; };
@@ -831,7 +965,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
         STAMP(2);
         // ---- phase 2
         if (crit) {
-            if (k + 1 < nf) {
+            if (k + 1 < nrows) {
                 const int s1 = slot(1), k1b = kb ^ 1;
                 // lanes 0..35: S_{k+1} = A_{k+1,k+1} - L_{k+1,k} A_{k+1,k}ᵀ
                 // lanes 36..41: y_{k+1} = b_{k+1} - L_{k+1,k} y_k
@@ -855,7 +989,8 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
                 const double I = gj_inverse6(M, lane, fail);
                 if (lane < 36) { Kv[k1b * 36 + lane] = I; ringK[kRK * 36 + lane] = I; }
                 else if (lane < 42) ringZ[kRK * 6 + lane - 36] = I;
-                if (fail && lane == 0) s_fail = 1;
+                // the look-ahead inverse past the last eliminated row (a separator row) is not a pivot
+                if (fail && lane == 0 && k + 1 < nsteps) s_fail = 1;
             }
         } else {
             // trailing update A_ij -= L_ik A_jkᵀ for all pairs (wi >= wj >= 1) except (1,1)
@@ -884,22 +1019,22 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
                 }
             }
             STAMP(6);
-            if (kR == R - 1 || k == nf - 1) {  // flush the staged steps k0..k to global
+            if (kR == R - 1 || k == nsteps - 1) {  // flush the staged steps k0..k to global
                 const int k0 = k - kR;
                 const int cnt = kR + 1;
                 if constexpr (BW >= 1)
                     for (int t = wt; t < cnt * BW * 36; t += NW) {
                         const int st = t / (BW * 36), rem = t % (BW * 36), w = 1 + rem / 36, e = rem % 36;
                         const int i = k0 + st + w;
-                        if (i < nf) d.Lband[((size_t)i * W + w) * 36 + e] = ringL[(size_t)st * BW * 36 + rem];
+                        if (i < nrows) g.Lband[((size_t)i * W + w) * 36 + e] = ringL[(size_t)st * BW * 36 + rem];
                     }
                 for (int t = wt; t < cnt * 36; t += NW)
-                    d.Kinv[(size_t)k0 * 36 + t] = ringK[((k0 + t / 36) % RK) * 36 + t % 36];
-                for (int t = wt; t < cnt * 6; t += NW) d.zb[(size_t)k0 * 6 + t] = ringZ[((k0 + t / 6) % RK) * 6 + t % 6];
+                    g.Kinv[(size_t)k0 * 36 + t] = ringK[((k0 + t / 36) % RK) * 36 + t % 36];
+                for (int t = wt; t < cnt * 6; t += NW) g.zb[(size_t)k0 * 6 + t] = ringZ[((k0 + t / 6) % RK) * 6 + t % 6];
             }
             STAMP(7);
             // block row k+W enters slot sk (row k is fully consumed)
-            const bool live = k + W < nf;
+            const bool live = k + W < nrows;
 #pragma unroll
             for (int q = 0; q < RFT; ++q) {
                 const int t = wt + q * NW;
@@ -915,36 +1050,117 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
         kRK = (kRK + 1 == RK) ? 0 : kRK + 1;
     }
 #ifdef PLBA_STAMPS
-    if ((tid & 63) == 0)
-        for (int q = 0; q < 8; ++q) atomicAdd(&d.stamps[(tid >> 6) * 8 + q], st_acc[q]);
+    if (stamps && (tid & 63) == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&stamps[(tid >> 6) * 8 + q], st_acc[q]);
 #endif
     __syncthreads();  // drains every wave's flush stores: the backward pass reads them
-    if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
-    if (s_fail) return;
-    // ---- backward: x_k = z_k - Σ_w L_{k+w,k}ᵀ x_{k+w}   (wave 0, no barriers; L prefetched)
-    if (tid < 64) {
-        const int lane = tid;
-        constexpr int kMaxB = (BW * 6 + 63) / 64 > 0 ? (BW * 6 + 63) / 64 : 1;
-        double Lc[kMaxB][6], Ln[kMaxB][6];
-        auto load_L = [&](int k, double (&dst)[kMaxB][6]) {
-            const int wmax = (k >= 0) ? min(BW, nf - 1 - k) : 0;
+    const bool failed = s_fail != 0;
+    if (g.sep && !failed) {  // rows nsteps..nsteps+BW-1 (all W blocks) and their right-hand sides
+        for (int t = tid; t < BW * W * 36; t += NT) {
+            const int i = t / (W * 36), rem = t % (W * 36);
+            g.sep[t] = win[(size_t)((sk + i) % W) * W * 36 + rem];
+        }
+        for (int t = tid; t < BW * 6; t += NT) g.sep[(size_t)BW * W * 36 + t] = bwin[((sk + t / 6) % W) * 6 + t % 6];
+    }
+    return failed;
+}
+
+// Backward substitution x_k = z_k - Σ_w L_{k+w,k}ᵀ x_{k+w} for k = nsteps-1..0, by ONE wave (no
+// barriers; L prefetched one step ahead). Rows nsteps..nsteps+BW-1 take x from `xsep` (a
+// separator solved elsewhere) or do not exist (xsep == nullptr, nsteps == nrows). Row k is
+// written to xp[k] (or xp[nf-1-k] for a reversed segment).
+// Right-looking variant for bw <= 10 (one lane per (row, component) of the BW-row window, all
+// in registers): once x_i is final, its 6 values are read from the owning lanes with
+// v_readlane and every window row j = i-w applies z_j -= L_{i,j}ᵀ x_i at once. The chain per
+// step is one readlane batch + one 6-term dot product; no LDS round trips.
+template <int BW>
+__device__ __forceinline__ void band_backward_rl(const double *Lband, const double *zb, int nsteps, int nrows,
+                                                 const double *xsep, double *xp, bool reversed, int nf, int lane) {
+    constexpr int W = BW + 1, kPipe = 4;
+    const int G = lane / 6, r = lane % 6;      // lane group G holds the window row j ≡ G (mod BW)
+    const bool act = lane < BW * 6;
+    const int top = xsep ? min(nrows - 1, nsteps - 1 + BW) : nsteps - 1;
+    // window rows top-BW+1..top: separator x (known) or z to be completed
+    double zv = 0.0;
+    if (act) {
+        int j = top - ((top - G) % BW + BW) % BW;  // the row of this group in [top-BW+1, top]
+        if (j >= 0) zv = j >= nsteps ? (xsep ? xsep[(j - nsteps) * 6 + r] : 0.0) : zb[(size_t)j * 6 + r];
+    }
+    double Lr[kPipe][6], zr[kPipe];
+    auto load_step = [&](int i, double (&dst)[6], double &z) {
+        // row i's L block for this lane's window row j = i - w, and z_{i-BW} for the group that
+        // takes row i-BW at step i
+        const int w = ((i - G - 1) % BW + BW) % BW + 1;
+        const bool ok = act && i >= 0 && i - w >= 0 && i - w < nsteps;
+        const double *L = Lband + ((size_t)max(i, 0) * W + w) * 36;
 #pragma unroll
-            for (int q = 0; q < kMaxB; ++q) {
-                const int t = q * 64 + lane;
-                const int w = 1 + t / 6, r = t % 6;
-                const bool ok = t < wmax * 6;
-                const double *L = d.Lband + ((size_t)(k + w) * W + w) * 36;
+        for (int m = 0; m < 6; ++m) dst[m] = ok ? L[m * 6 + r] : 0.0;
+        z = (act && i - BW >= 0 && i - BW < nsteps) ? zb[(size_t)(i - BW) * 6 + r] : 0.0;
+    };
 #pragma unroll
-                for (int m = 0; m < 6; ++m) dst[q][m] = ok ? L[m * 6 + r] : 0.0;
+    for (int u = 0; u < kPipe; ++u) load_step(top - u, Lr[u], zr[u]);
+    for (int ib = top; ib >= 0; ib -= kPipe) {
+#pragma unroll
+        for (int u = 0; u < kPipe; ++u) {
+            const int i = ib - u;
+            if (i < 0) break;
+            const int gi = i % BW;             // group holding row i (final)
+            double x[6];
+#pragma unroll
+            for (int m = 0; m < 6; ++m) {
+                const int src = gi * 6 + m;
+                const int lo = __builtin_amdgcn_readlane(__double2loint(zv), src);
+                const int hi = __builtin_amdgcn_readlane(__double2hiint(zv), src);
+                x[m] = __hiloint2double(hi, lo);
             }
-        };
-        load_L(nf - 1, Lc);
-        double zc = (lane < 6) ? d.zb[(size_t)(nf - 1) * 6 + lane] : 0.0, zn;
-        for (int k = nf - 1; k >= 0; --k) {
-            const int wmax = min(BW, nf - 1 - k);
-            load_L(k - 1, Ln);
-            zn = (lane < 6 && k > 0) ? d.zb[(size_t)(k - 1) * 6 + lane] : 0.0;
-            const double zk = zc;
+            if (G == gi && act) {
+                if (i < nsteps) xp[(size_t)(reversed ? nf - 1 - i : i) * 6 + r] = zv;
+                zv = zr[u];                    // this group now holds row i-BW
+            }
+            // z_j -= L_{i,j}ᵀ x_i for the window rows j < nsteps (Lr is zero elsewhere)
+            double acc = 0.0;
+#pragma unroll
+            for (int m = 0; m < 6; ++m) acc = fma(Lr[u][m], x[m], acc);
+            zv -= acc;
+            load_step(i - kPipe, Lr[u], zr[u]);
+        }
+    }
+}
+
+template <int BW>
+__device__ __forceinline__ void band_backward(const double *Lband, const double *zb, int nsteps, int nrows, const double *xsep,
+                              double *xp, bool reversed, int nf, double *xr, double *part, int lane) {
+    constexpr int W = BW + 1;
+    const int last = min(nrows - 1, nsteps - 1 + BW);  // highest row coupled to the segment
+    if (xsep && lane < 6)
+        for (int i = 0; i < BW && nsteps + i < nrows; ++i) xr[((nsteps + i) % W) * 6 + lane] = xsep[i * 6 + lane];
+    wave_lds_sync();
+    // L_{k+w,k} and z_k are loaded kPipe steps ahead into a register ring (static slots: the
+    // step loop is unrolled by kPipe), so their L2 latency hides behind kPipe steps of work
+    constexpr int kMaxB = (BW * 6 + 63) / 64 > 0 ? (BW * 6 + 63) / 64 : 1;
+    constexpr int kPipe = kMaxB == 1 ? 6 : 2;  // register budget: 12 f64 per slot per lane at bw <= 10
+    double Lr[kPipe][kMaxB][6], zr[kPipe];
+    auto load_step = [&](int k, double (&dst)[kMaxB][6], double &z) {
+        const int wmax = (k >= 0) ? min(BW, last - k) : 0;
+#pragma unroll
+        for (int q = 0; q < kMaxB; ++q) {
+            const int t = q * 64 + lane;
+            const int w = 1 + t / 6, r = t % 6;
+            const bool ok = t < wmax * 6;
+            const double *L = Lband + ((size_t)(k + w) * W + w) * 36;
+#pragma unroll
+            for (int m = 0; m < 6; ++m) dst[q][m] = ok ? L[m * 6 + r] : 0.0;
+        }
+        z = (lane < 6 && k >= 0) ? zb[(size_t)k * 6 + lane] : 0.0;
+    };
+#pragma unroll
+    for (int u = 0; u < kPipe; ++u) load_step(nsteps - 1 - u, Lr[u], zr[u]);
+    for (int kb = nsteps - 1; kb >= 0; kb -= kPipe) {
+#pragma unroll
+        for (int u = 0; u < kPipe; ++u) {
+            const int k = kb - u;
+            if (k < 0) break;
+            const int wmax = min(BW, last - k);
 #pragma unroll
             for (int q = 0; q < kMaxB; ++q) {
                 const int t = q * 64 + lane;
@@ -953,70 +1169,211 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
                     const double *x = xr + (i % W) * 6;
                     double s = 0.0;
 #pragma unroll
-                    for (int m = 0; m < 6; ++m) s += Lc[q][m] * x[m];
+                    for (int m = 0; m < 6; ++m) s += Lr[u][q][m] * x[m];
                     part[w * 6 + r] = s;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
             if (lane < 6) {
-                double v = zk;
+                double v = zr[u];
                 for (int w = 1; w <= wmax; ++w) v -= part[w * 6 + lane];
                 xr[(k % W) * 6 + lane] = v;
-                d.xp[(size_t)k * 6 + lane] = v;
+                xp[(size_t)(reversed ? nf - 1 - k : k) * 6 + lane] = v;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int q = 0; q < kMaxB; ++q)
-#pragma unroll
-                for (int m = 0; m < 6; ++m) Lc[q][m] = Ln[q][m];
-            zc = zn;
+            wave_lds_sync();
+            load_step(k - kPipe, Lr[u], zr[u]);  // refill this slot kPipe steps ahead
         }
     }
+}
+
+template <int BW>
+__global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
+    TRIAL_GUARD
+    extern __shared__ double lds[];
+    const BandSeg g{d.Bd, d.bs, d.Lband, d.Kinv, d.zb, d.nf, d.nf, nullptr};
+    const bool fail = band_forward<BW>(g, lds, d.ring, d.stamps);
+    if (threadIdx.x == 0) d.ctrl->solve_ok = fail ? 0 : 1;
+    if (!fail && threadIdx.x < 64) {
+        double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
+        band_lds<BW>(lds, d.ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
+        if constexpr (BW >= 1 && BW * 6 <= 64) band_backward_rl<BW>(d.Lband, d.zb, d.nf, d.nf, nullptr, d.xp, false, d.nf, threadIdx.x);
+        else band_backward<BW>(d.Lband, d.zb, d.nf, d.nf, nullptr, d.xp, false, d.nf, xr, part, threadIdx.x);
+    }
+    __syncthreads();
+    pose_update_wg<kBandNT>(d);  // applied even after a failed solve, with the previous x_p (A13)
+}
+
+// Two-sided ("twisted") banded LDLᵀ: workgroup 0 eliminates block rows 0..m-1 top-down,
+// workgroup 1 eliminates rows nf-1..m+BW bottom-up (as the top-down elimination of the
+// block-reversed matrix Bd2), concurrently on two CUs. The two eliminated sets do not couple
+// (they are > BW blocks apart), so their Schur updates of the BW-block separator m..m+BW-1
+// add: S_sep = W0 + W1 − A_sep. The workgroup that finishes second solves the separator
+// (dense Gauss–Jordan, no pivoting: the pivots are LDLᵀ pivots, a zero one fails the solve as
+// SimplicialLDLT does) and runs both back substitutions on two waves. Half the serial chain.
+template <int BW>
+__device__ __forceinline__ void k_rcs_factor_twisted_body(Dev &d) {
+    TRIAL_GUARD
+    constexpr int W = BW + 1, NT = kBandNT, NS = 6 * BW, LD = NS + 1;
+    extern __shared__ double lds[];
+    __shared__ int s_last, s_sfail;
+    const int seg = blockIdx.x, tid = threadIdx.x;
+    const size_t sep_stride = (size_t)BW * W * 36 + (size_t)BW * 6;
+    const int m = d.tw_m, n1 = d.nf - BW - d.tw_m;
+    const BandSeg g = seg == 0 ? BandSeg{d.Bd, d.bs, d.Lband, d.Kinv, d.zb, d.nf, m, d.tw_sep}
+                               : BandSeg{d.Bd2, d.bs2, d.Lband2, d.Kinv2, d.zb2, d.nf, n1, d.tw_sep + sep_stride};
+#ifdef PLBA_STAMPS
+    unsigned long long tw_t0 = __builtin_readcyclecounter();
+#endif
+    const bool fail = band_forward<BW>(g, lds, d.ring, seg == 0 ? d.stamps : nullptr);
+#ifdef PLBA_STAMPS
+    unsigned long long tw_t1 = __builtin_readcyclecounter();
+#define TW_MARK(q, t)                                                     \
+    do {                                                                  \
+        if (tid == 0) atomicAdd(&d.stamps[16 * 8 + (q)], (t));            \
+    } while (0)
+    if (seg == 0) TW_MARK(0, tw_t1 - tw_t0); else TW_MARK(1, tw_t1 - tw_t0);
+#else
+#define TW_MARK(q, t) do {} while (0)
+#endif
+    // publish (release): every thread's L / z / separator stores, then the arrival counter
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        atomicExch(&d.tw_fail[seg], fail ? 1 : 0);
+        __threadfence();
+        s_last = atomicAdd(d.tw_count, 1) == 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: the other workgroup's stores are visible from here on
+    if (tid == 0) {
+        atomicExch(d.tw_count, 0);  // ready for the next launch
+        s_sfail = (atomicAdd(&d.tw_fail[0], 0) | atomicAdd(&d.tw_fail[1], 0)) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_sfail) {
+    double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
+    band_lds<BW>(lds, d.ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
+    double *xr1 = lds + band_lds_doubles(BW, d.ring), *part1 = xr1 + W * 6;
+    double *Ms = part1 + W * 6, *fcol = Ms + (size_t)NS * LD;
+    // ---- separator system S_sep (lower block (i,j), i >= j, w = i-j) and its right-hand side
+    const double *W0 = d.tw_sep, *W1 = d.tw_sep + sep_stride;
+    for (int t = tid; t < NS * NS; t += NT) {
+        const int R_ = t / NS, C_ = t % NS;
+        const int hi = R_ >= C_ ? R_ : C_, lo = R_ >= C_ ? C_ : R_;   // lower-triangle entry (hi, lo)
+        const int i = hi / 6, a = hi % 6, j = lo / 6, b = lo % 6, w = i - j;
+        double v;
+        if (w > BW) v = 0.0;
+        else {
+            const double w0 = W0[((size_t)i * W + w) * 36 + a * 6 + b];
+            const double w1 = W1[((size_t)(BW - 1 - j) * W + w) * 36 + b * 6 + a];
+            const double a0 = d.Bd[((size_t)(m + i) * W + w) * 36 + a * 6 + b];
+            v = w0 + w1 - a0;
+        }
+        Ms[(size_t)R_ * LD + C_] = v;
+    }
+    for (int t = tid; t < NS; t += NT) {
+        const int i = t / 6, a = t % 6;
+        Ms[(size_t)t * LD + NS] = W0[(size_t)BW * W * 36 + i * 6 + a] + W1[(size_t)BW * W * 36 + (BW - 1 - i) * 6 + a] -
+                                  d.bs[(size_t)(m + i) * 6 + a];
+    }
+    if (tid == 0) s_sfail = 0;
+    __syncthreads();
+    // block Gauss–Jordan with 6x6 pivots: wave 0 inverts the pivot block (its scalar pivots are
+    // the LDLᵀ pivots), then every other block row is eliminated in one parallel pass
+    double *Kp = fcol, *Fb = Kp + (size_t)BW * 36;  // [BW][36] pivot inverses, [BW][36] factors
+    for (int P = 0; P < BW; ++P) {
+        if (tid < 64) {
+            bool f = false;
+            const double M = tid < 36 ? Ms[(size_t)(P * 6 + tid / 6) * LD + P * 6 + tid % 6] : 0.0;
+            const double I = gj_inverse6(M, tid, f);
+            if (tid < 36) Kp[P * 36 + tid] = I;
+            if (f && tid == 0) s_sfail = 1;
+        }
+        __syncthreads();
+        if (s_sfail) break;
+        for (int t = tid; t < BW * 36; t += NT) {  // F_I = A_IP · A_PP⁻¹
+            const int I = t / 36, e = t % 36, a_ = e / 6, b_ = e % 6;
+            if (I == P) continue;
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) acc = fma(Ms[(size_t)(I * 6 + a_) * LD + P * 6 + q], Kp[P * 36 + q * 6 + b_], acc);
+            Fb[t] = acc;
+        }
+        __syncthreads();
+        const int ncol = LD - P * 6;
+        for (int t = tid; t < NS * ncol; t += NT) {  // A_Ij -= F_I · A_Pj  (j >= pivot columns)
+            const int row = t / ncol, j = P * 6 + t % ncol, I = row / 6, a_ = row % 6;
+            if (I == P) continue;
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) acc = fma(Fb[I * 36 + a_ * 6 + q], Ms[(size_t)(P * 6 + q) * LD + j], acc);
+            Ms[(size_t)row * LD + j] -= acc;
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+#ifdef PLBA_STAMPS
+    unsigned long long tw_t2 = __builtin_readcyclecounter();
+    TW_MARK(2, tw_t2 - tw_t1);
+#endif
+    if (!s_sfail) {
+    // x_sep in both segment orders (fcol is free now): rows m+i for segment 0, reversed rows
+    // n1+i = original m+BW-1-i for segment 1
+    double *xs0 = Fb;  // factors are free now
+    for (int t = tid; t < NS; t += NT) {  // x_P = A_PP⁻¹ rhs_P (block rows are decoupled now)
+        const int P = t / 6, a_ = t % 6;
+        double x = 0.0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) x = fma(Kp[P * 36 + a_ * 6 + q], Ms[(size_t)(P * 6 + q) * LD + NS], x);
+        xs0[t] = x;
+        d.xp[(size_t)m * 6 + t] = x;
+    }
+    __syncthreads();
+    double *xsr = Ms;  // reversed-order copy (Ms is no longer needed)
+    for (int t = tid; t < NS; t += NT) xsr[t] = xs0[(BW - 1 - t / 6) * 6 + t % 6];
+    __syncthreads();
+    if constexpr (BW * 6 <= 64) {
+        if (tid < 64) band_backward_rl<BW>(d.Lband, d.zb, m, d.nf, xs0, d.xp, false, d.nf, tid);
+        else if (tid < 128) band_backward_rl<BW>(d.Lband2, d.zb2, n1, d.nf, xsr, d.xp, true, d.nf, tid - 64);
+    } else {
+        if (tid < 64) band_backward<BW>(d.Lband, d.zb, m, d.nf, xs0, d.xp, false, d.nf, xr, part, tid);
+        else if (tid < 128) band_backward<BW>(d.Lband2, d.zb2, n1, d.nf, xsr, d.xp, true, d.nf, xr1, part1, tid - 64);
+    }
+#ifdef PLBA_STAMPS
+    if (tid == 0) TW_MARK(3, __builtin_readcyclecounter() - tw_t2);
+    if (tid == 0) TW_MARK(4, 1);
+#endif
+    }  // separator solved
+    }  // both segments eliminated
+#undef TW_MARK
+    __syncthreads();
+    if (tid == 0) d.ctrl->solve_ok = s_sfail ? 0 : 1;
+    pose_update_wg<NT>(d);  // applied even after a failed solve, with the previous x_p (A13)
+}
+
+template <int BW>
+__global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d) {
+    if constexpr (BW >= 1) k_rcs_factor_twisted_body<BW>(d);  // (the host never selects bw 0)
 }
 
 // ---------------------------------------------------------------- update + trial evaluation
+// stand-alone pose update (windows without free poses: no factorisation kernel to fuse into)
 __global__ __launch_bounds__(kBlock) void k_pose_update(Dev d) {
     TRIAL_GUARD
-    __shared__ double sh[kBlock / 64];
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    double sc = 0.0;
-    if (k < d.n_kf) {
-        const double *Tc = d.T_cur + (size_t)k * 12;
-        double *Tt = d.T_trial + (size_t)k * 12;
-        const int h = d.kf_hidx[k];
-        // sharded: a pose's activity is global (another rank may hold its edges); a free pose
-        // with no active edge anywhere has a zero RCS row, x = 0 and an exact identity oplus
-        if (h >= 0 && (d.sharded || d.kf_active[k])) {
-            const double lam = d.ctrl->lambda;
-            double x[6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                x[i] = d.xp[6 * h + i];
-                sc += x[i] * (lam * x[i] + d.bp[(size_t)h * 6 + i]);
-            }
-            pose_oplus(Tc, x, Tt);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 12; ++i) Tt[i] = Tc[i];
-        }
-    }
-    double s = block_sum<kBlock>(sc, sh);
-    if (threadIdx.x == 0) d.part_ps[blockIdx.x] = s;
+    if (blockIdx.x == 0) pose_update_wg<kBlock>(d);
 }
 
 // ---------------------------------------------------------------- edge-parallel trial path
-// per landmark: (Hll + λI) = L Lᵀ, g = L⁻¹ b_l
-__global__ __launch_bounds__(kBlock) void k_lm_chol(Dev d) {
-    TRIAL_GUARD
-    const int l = blockIdx.x * kBlock + threadIdx.x;
-    if (l >= d.n_lm) return;
-    const double lam = d.ctrl->lambda;
+// per landmark: (Hll + λI) = L Lᵀ, g = L⁻¹ b_l (packed lower; recomputed where needed — 4x4,
+// cheaper than a kernel boundary)
+__device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, double (&L)[10], double (&g)[4]) {
     const int DIM = is_point_lm(d, l) ? 3 : 4;
-    double H[10], L[10], g[4] = {0, 0, 0, 0};
+    double H[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) { H[k] = d.Hll[(size_t)l * 10 + k]; L[k] = 0.0; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] = 0.0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         if (j < DIM) {
@@ -1045,10 +1402,6 @@ __global__ __launch_bounds__(kBlock) void k_lm_chol(Dev d) {
             g[i] = t / L[pk(i, i)];
         }
     }
-#pragma unroll
-    for (int k = 0; k < 10; ++k) d.Lc[(size_t)l * 10 + k] = L[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) d.gv[(size_t)l * 4 + k] = g[k];
 }
 // per edge: Z_e = B_e L⁻ᵀ (rows solved with L), q_e = Z_e g
 __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
@@ -1058,10 +1411,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
     const int l = d.e_lm[e];
     const int DIM = e < d.Ep ? 3 : 4;
     double L[10], g[4], B[8];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) L[k] = d.Lc[(size_t)l * 10 + k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) g[k] = d.gv[(size_t)l * 4 + k];
+    lm_chol(d, l, d.ctrl->lambda, L, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) B[k] = d.B[(size_t)e * 8 + k];
     double z[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -1088,29 +1438,6 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
     d.q[(size_t)e * 2 + 0] = q0;
     d.q[(size_t)e * 2 + 1] = q1;
 }
-// per edge: u_e = B_eᵀ (A_e x_p)
-__global__ __launch_bounds__(kBlock) void k_edge_backsub(Dev d) {
-    TRIAL_GUARD
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    if (e >= d.E || !d.ctrl->solve_ok) return;
-    const int h = d.e_hidx[e];
-    double u[4] = {0, 0, 0, 0};
-    if (h >= 0) {
-        const double *A = d.A + (size_t)e * 12;
-        const double *B = d.B + (size_t)e * 8;
-        double ax0 = 0, ax1 = 0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const double xk = d.xp[6 * h + k];
-            ax0 += A[k] * xk;
-            ax1 += A[6 + k] * xk;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) u[i] = B[i] * ax0 + B[4 + i] * ax1;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) d.ue[(size_t)e * 4 + i] = u[i];
-}
 // per landmark: x_l = L⁻ᵀ L⁻¹ (b_l - Σ u_e), oplus into the trial state, scale partial
 __global__ __launch_bounds__(kBlock) void k_lm_solve(Dev d) {
     TRIAL_GUARD
@@ -1118,23 +1445,35 @@ __global__ __launch_bounds__(kBlock) void k_lm_solve(Dev d) {
     const int l = blockIdx.x * kBlock + threadIdx.x;
     double sc = 0.0;
     if (l < d.n_lm) {
-        const double *Xc = d.X_cur + (size_t)l * 4;
-        double *Xt = d.X_trial + (size_t)l * 4;
+        const double *Xc = Xcur(d) + (size_t)l * 4;
+        double *Xt = Xtrial(d) + (size_t)l * 4;
         if (d.lm_active[l]) {
             const bool pt = is_point_lm(d, l);
             const int DIM = pt ? 3 : 4;
             const double lam = d.ctrl->lambda;
             double x[4] = {0, 0, 0, 0};
             if (d.ctrl->solve_ok) {
+                // r = b_l − Σ_e Hpl_eᵀ x_p,  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)  (edges of a fixed pose: 0)
                 double r[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) r[i] = d.bl[(size_t)l * 4 + i];
-                for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e)
+                for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
+                    const int h = d.e_hidx[e];
+                    if (h < 0) continue;
+                    const double *A = d.A + (size_t)e * 12;
+                    const double *Bm = d.B + (size_t)e * 8;
+                    double ax0 = 0, ax1 = 0;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) r[i] -= d.ue[(size_t)e * 4 + i];
-                double L[10], y[4] = {0, 0, 0, 0};
+                    for (int k = 0; k < 6; ++k) {
+                        const double xk = d.xp[6 * h + k];
+                        ax0 += A[k] * xk;
+                        ax1 += A[6 + k] * xk;
+                    }
 #pragma unroll
-                for (int k = 0; k < 10; ++k) L[k] = d.Lc[(size_t)l * 10 + k];
+                    for (int i = 0; i < 4; ++i) r[i] -= Bm[i] * ax0 + Bm[4 + i] * ax1;
+                }
+                double L[10], gl[4], y[4] = {0, 0, 0, 0};
+                lm_chol(d, l, lam, L, gl);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     if (i < DIM) {
@@ -1190,12 +1529,12 @@ __global__ __launch_bounds__(kBlock) void k_edge_eval(Dev d) {
     double chi = 0.0;
     if (e < d.E && d.e_active[e]) {
         const int l = d.e_lm[e];
-        const double *T = d.T_trial + (size_t)d.e_kf[e] * 12;
+        const double *T = Ttrial(d) + (size_t)d.e_kf[e] * 12;
         const double *obs = d.e_obs + (size_t)e * 4;
         double err[2], delta;
         if (e < d.Ep) {
             double z;
-            point_error(T, d.X_trial + (size_t)l * 4, obs, d.cam, err, z);
+            point_error(T, Xtrial(d) + (size_t)l * 4, obs, d.cam, err, z);
             delta = d.huber_pt;
         } else {
             line_error(T, d.Xplk + (size_t)l * 6, obs, d.cam, err);
@@ -1269,7 +1608,7 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
         if (!isfinite(c->lambda)) c->broke = 1;
         else c->qmax += 1;
     }
-    c->commit_pending = c->accept;
+    if (c->accept) c->cur ^= 1;  // the trial becomes the current estimate
     const bool again = !c->broke && rho < 0 && c->qmax < c->max_trials;
     if (again) return;  // another damped trial of this iteration
     // end of OptimizationAlgorithmLevenberg::solve(iter)
@@ -1288,85 +1627,13 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_commit(Dev d) {
-    if (!d.ctrl->commit_pending) return;
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < d.n_kf && d.kf_hidx[i] >= 0 && (d.sharded || d.kf_active[i])) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) d.T_cur[(size_t)i * 12 + k] = d.T_trial[(size_t)i * 12 + k];
-    }
-    if (i < d.n_lm && d.lm_active[i]) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d.X_cur[(size_t)i * 4 + k] = d.X_trial[(size_t)i * 4 + k];
-    }
-}
-
-// ---------------------------------------------------------------- stage switch (initializeOptimization)
-// classification before a stage (src/mapHandler.cpp:6125-6147): level |= (χ² > thr || depth <= 0)
-__global__ void k_switch_classify(Dev d, double thr) {
-    const Ctrl *c = d.ctrl;
-    if (!c->switch_pending || !c->stage_classify[c->stage + 1]) return;
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= d.E) return;
-    bool bad = d.chi2_last[e] > thr;
-    if (e < d.Ep) {
-        double Pc[3];
-        point_pc(d.T_cur + (size_t)d.e_kf[e] * 12, d.X_cur + (size_t)d.e_lm[e] * 4, Pc);
-        bad = bad || !(Pc[2] > 0.0);
-    }
-    if (bad) d.e_level[e] = 1;
-}
-__global__ void k_switch_clear(Dev d) {
-    const Ctrl *c = d.ctrl;
-    if (!c->switch_pending) return;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < d.n_lm) d.lm_active[i] = 0;
-    if (i < d.n_kf) d.kf_active[i] = 0;
-    if (i == 0) d.ctrl->any_active = 0;
-}
-// an edge is active iff its level is the optimised level (landmarks are never fixed); a vertex
-// iff it has an active edge (SparseOptimizer::initializeOptimization)
-__global__ void k_switch_activate(Dev d) {
-    Ctrl *c = d.ctrl;
-    if (!c->switch_pending) return;
-    const int lvl = c->stage_level[c->stage + 1];
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    bool act = false;
-    if (e < d.E) {
-        act = d.e_level[e] == lvl;
-        d.e_active[e] = act ? 1 : 0;
-        if (act) {
-            d.lm_active[d.e_lm[e]] = 1;
-            d.kf_active[d.e_kf[e]] = 1;
-        }
-    }
-    if (__ballot(act) && (threadIdx.x & 63) == 0) atomicOr(&c->any_active, 1);
-}
-__global__ void k_switch_finish(Dev d) {
-    Ctrl *c = d.ctrl;
-    if (!c->switch_pending || threadIdx.x != 0) return;
-    c->switch_pending = 0;
-    c->stage += 1;
-    c->iter = 0;
-    c->robust = c->stage_robust[c->stage];
-    c->level = c->stage_level[c->stage];
-    if (!c->any_active && !d.sharded) {  // _ivMap empty: optimize() returns -1 without iterating
-        c->iters_done[c->stage] = -1;
-        c->chi2_final[c->stage] = 0.0;
-        if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
-        else c->all_done = 1;
-    } else {
-        c->need_iter = 1;
-    }
-}
-
 // ---------------------------------------------------------------- outlier pass helpers
 // computeError() at the current state for edges of `level`
 __global__ void k_refresh(Dev d, int level) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= d.E || d.e_level[e] != level) return;
-    const double *T = d.T_cur + (size_t)d.e_kf[e] * 12;
-    const double *X = d.X_cur + (size_t)d.e_lm[e] * 4;
+    const double *T = Tcur(d) + (size_t)d.e_kf[e] * 12;
+    const double *X = Xcur(d) + (size_t)d.e_lm[e] * 4;
     const double *obs = d.e_obs + (size_t)e * 4;
     double err[2];
     if (e < d.Ep) {
@@ -1385,7 +1652,7 @@ __global__ void k_depth(Dev d, uint8_t *out) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= d.Ep) return;
     double Pc[3];
-    point_pc(d.T_cur + (size_t)d.e_kf[e] * 12, d.X_cur + (size_t)d.e_lm[e] * 4, Pc);
+    point_pc(Tcur(d) + (size_t)d.e_kf[e] * 12, Xcur(d) + (size_t)d.e_lm[e] * 4, Pc);
     out[e] = Pc[2] > 0.0 ? 1 : 0;
 }
 
@@ -1395,7 +1662,7 @@ __global__ void k_gather(Dev d, const uint8_t *depth) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < d.n_lm)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d.gat[(size_t)d.lm_gpos[i] * 4 + k] = d.X_cur[(size_t)i * 4 + k];
+        for (int k = 0; k < 4; ++k) d.gat[(size_t)d.lm_gpos[i] * 4 + k] = Xcur(d)[(size_t)i * 4 + k];
     if (i < d.E) {
         double *o = d.gat + (size_t)d.n_lm_g * 4;
         const int g = d.e_gpos[i];

@@ -105,6 +105,25 @@ def test_wide_bands_and_dense_fallback(solver, tmax, n_kf):
     assert st["banded"] == (1 if tmax <= 20 else 0), st
 
 
+@pytest.mark.parametrize("cfg,kw", [("C2", {}), ("C1", dict(n_kf=60, n_pt=1500, seed=77, track_max=12))])
+def test_twisted_factorisation_matches_single_sweep(solver, monkeypatch, cfg, kw):
+    # two-sided band LDLᵀ (2 workgroups + separator) vs the one-sided sweep, both vs the oracle;
+    # the second case has bw 11 (separator solved by the multi-wave Gauss–Jordan)
+    g = synth.generate(cfg, **kw)
+    ref = oa.lba_plucker(g)
+    solver.upload(g)
+    assert solver.structure_stats()["twisted"] == 1
+    tw = solver.lba_plucker()
+    _check(tw, ref)
+    monkeypatch.setenv("PLBA_NO_TWIST", "1")
+    solver.upload(g)
+    assert solver.structure_stats()["twisted"] == 0
+    one = solver.lba_plucker()
+    _check(one, ref)
+    monkeypatch.delenv("PLBA_NO_TWIST")
+    assert np.abs(tw["kf_Tcw"] - one["kf_Tcw"]).max() < 1e-10
+
+
 def test_empty_graph(solver):
     g = synth.generate("C1", n_pt=0, n_ln=0)
     out, ref = _run(solver, g)
