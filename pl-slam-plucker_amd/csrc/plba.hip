@@ -76,6 +76,7 @@ struct plba_ctx {
     // host-side bookkeeping
     int32_t n_kf = 0, n_pt = 0, n_ln = 0, Ep = 0, El = 0;
     std::vector<int32_t> e_orig;        // CSR edge -> original index within its type
+    std::vector<int32_t> lm_gpos;       // local landmark -> whole-window landmark (points, then lines)
     std::vector<uint8_t> h_level;       // [E] CSR order
     std::vector<plba_iter_trace> trace;
     int stage = 0;
@@ -299,12 +300,32 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // landmarks owned by this rank (all of them unless the window is sharded)
     std::vector<int32_t> pt_owner(n_pt_g, 0), ln_owner(n_ln_g, 0);
     if (R > 1) shard_plan(g, R, pt_owner.data(), ln_owner.data());
+    // Local landmark order: points then lines, each sorted (stably) by the id rank of the
+    // keyframe of their first observation, so the edges of one pose — and the landmarks one RCS
+    // block couples — sit in a narrow range of the landmark-major edge array (cache locality of
+    // the pose reduction and the Schur assembly; any order gives the same solution).
     std::vector<int32_t> pt_loc(n_pt_g, -1), ln_loc(n_ln_g, -1), lm_gpos;
     int n_pt = 0, n_ln = 0;
-    for (int p = 0; p < n_pt_g; ++p)
-        if (pt_owner[p] == rank) { pt_loc[p] = n_pt++; lm_gpos.push_back(p); }
-    for (int l = 0; l < n_ln_g; ++l)
-        if (ln_owner[l] == rank) { ln_loc[l] = n_ln++; lm_gpos.push_back(n_pt_g + l); }
+    {
+        std::vector<int32_t> korder_(n_kf), kpos(n_kf);
+        std::iota(korder_.begin(), korder_.end(), 0);
+        std::stable_sort(korder_.begin(), korder_.end(), [&](int a, int b) { return g->kf_id[a] < g->kf_id[b]; });
+        for (int i = 0; i < n_kf; ++i) kpos[korder_[i]] = i;
+        std::vector<int32_t> key_pt(n_pt_g, INT32_MAX), key_ln(n_ln_g, INT32_MAX);
+        for (int e = Ep_g - 1; e >= 0; --e) key_pt[g->ept_lm[e]] = kpos[g->ept_kf[e]];
+        for (int e = El_g - 1; e >= 0; --e) key_ln[g->eln_lm[e]] = kpos[g->eln_kf[e]];
+        std::vector<int32_t> ord;
+        for (int p = 0; p < n_pt_g; ++p)
+            if (pt_owner[p] == rank) ord.push_back(p);
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key_pt[a] < key_pt[b]; });
+        for (int p : ord) { pt_loc[p] = n_pt++; lm_gpos.push_back(p); }
+        ord.clear();
+        for (int l = 0; l < n_ln_g; ++l)
+            if (ln_owner[l] == rank) ord.push_back(l);
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key_ln[a] < key_ln[b]; });
+        for (int l : ord) { ln_loc[l] = n_ln++; lm_gpos.push_back(n_pt_g + l); }
+    }
+    ctx->lm_gpos = lm_gpos;
     int Ep = 0, El = 0;
     for (int e = 0; e < Ep_g; ++e) Ep += pt_loc[g->ept_lm[e]] >= 0;
     for (int e = 0; e < El_g; ++e) El += ln_loc[g->eln_lm[e]] >= 0;
@@ -690,7 +711,7 @@ int launch_step(plba_ctx *ctx) {
     hipStream_t s = ctx->stream;
     const int nv = std::max(std::max(d.n_lm, d.n_kf), 1);
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
-    if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kBlock), 0, s, d));
+    if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kPoseNT), 0, s, d));
     if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
     if (d.sharded) {
         LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kBlock), 0, s, d));
@@ -1039,12 +1060,15 @@ int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth
         PLBA_CHECK(hipMemcpyAsync(kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost, ctx->stream));
     if (d.n_lm) PLBA_CHECK(hipMemcpyAsync(X.data(), d.Xb[ctx->cur], sizeof(double) * X.size(), hipMemcpyDeviceToHost, ctx->stream));
     PLBA_CHECK(hipStreamSynchronize(ctx->stream));
-    if (pt_xyz)
-        for (int p = 0; p < d.n_pt; ++p)
-            for (int k = 0; k < 3; ++k) pt_xyz[3 * p + k] = X[(size_t)p * 4 + k];
-    if (ln_orth)
-        for (int l = 0; l < d.n_ln; ++l)
-            for (int k = 0; k < 4; ++k) ln_orth[4 * l + k] = X[(size_t)(d.n_pt + l) * 4 + k];
+    for (int i = 0; i < d.n_lm; ++i) {
+        const int gp = ctx->lm_gpos[i];
+        if (gp < ctx->n_pt) {
+            if (pt_xyz)
+                for (int k = 0; k < 3; ++k) pt_xyz[3 * (size_t)gp + k] = X[(size_t)i * 4 + k];
+        } else if (ln_orth) {
+            for (int k = 0; k < 4; ++k) ln_orth[4 * (size_t)(gp - ctx->n_pt) + k] = X[(size_t)i * 4 + k];
+        }
+    }
     return PLBA_OK;
 }
 

@@ -291,13 +291,14 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
 }
 
 // one workgroup per free pose: Hpp = Σ AᵀA, b_p = Σ Aᵀc (deterministic)
-__global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
+constexpr int kPoseNT = 256;
+__global__ __launch_bounds__(kPoseNT) void k_pose_reduce(Dev d) {
     ITER_GUARD
     const int h = blockIdx.x;
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-    for (int p = d.pe_off[h] + threadIdx.x; p < d.pe_off[h + 1]; p += kBlock) {
+    for (int p = d.pe_off[h] + threadIdx.x; p < d.pe_off[h + 1]; p += kPoseNT) {
         const int e = d.pe_list[p];
         const double *A = d.A + (size_t)e * 12;
         const double *c = d.cvec + (size_t)e * 2;
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
 #pragma unroll
         for (int r = 0; r < 6; ++r) acc[21 + r] += a0[r] * c0 + a1[r] * c1;
     }
-    __shared__ double sh27[kBlock / 64][27];
+    __shared__ double sh27[kPoseNT / 64][27];
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = wave_sum(acc[k]);
     if ((threadIdx.x & 63) == 0)
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(kBlock) void k_pose_reduce(Dev d) {
     if (threadIdx.x == 0)
         for (int k = 0; k < 27; ++k) {
             double v = sh27[0][k];
-            for (int w = 1; w < kBlock / 64; ++w) v += sh27[w][k];
+            for (int w = 1; w < kPoseNT / 64; ++w) v += sh27[w][k];
             out[k] = v;
         }
     if (threadIdx.x == 0) {
@@ -479,7 +480,13 @@ __global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
 __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
     TRIAL_GUARD
     __shared__ double red[64][43];
-    const int ch = blockIdx.x, lane = threadIdx.x;
+    // XCD-aware remap (blocks are dealt round-robin over the 8 XCDs): each XCD gets a contiguous
+    // run of chunks = a contiguous range of RCS block rows, so the A/Z rows of the landmarks
+    // they couple are re-read from that XCD's L2 instead of the fabric (speed only)
+    const int nb = gridDim.x, per = (nb + 7) / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int full = nb - 8 * (per - 1);  // XCDs that get `per` chunks (the rest get per-1)
+    const int ch = xcd < full ? xcd * per + slot : full * per + (xcd - full) * (per - 1) + slot;
+    const int lane = threadIdx.x;
     const int b = d.ch_blk[ch];
     const bool diag = d.blk_i1[b] == d.blk_i2[b];
     double acc[42];
@@ -1235,22 +1242,27 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(Dev &d) {
 #else
 #define TW_MARK(q, t) do {} while (0)
 #endif
-    // publish (release): every thread's L / z / separator stores, then the arrival counter
-    __threadfence();
+    // hand-off (MI355X_MICROARCH.md §Workgroup dispatch…, counter form): every wave drains its
+    // L / z / separator stores, one agent release by lane 0, then the arrival counter; the
+    // workgroup whose add returns 1 is last and acquires once before reading the other's data
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        atomicExch(&d.tw_fail[seg], fail ? 1 : 0);
-        __threadfence();
-        s_last = atomicAdd(d.tw_count, 1) == 1;
+        __hip_atomic_store(&d.tw_fail[seg], fail ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(d.tw_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == 1 ? 1 : 0;
+        if (old == 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(d.tw_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+            s_sfail = (__hip_atomic_load(&d.tw_fail[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                       __hip_atomic_load(&d.tw_fail[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? 1 : 0;
+        }
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();  // acquire: the other workgroup's stores are visible from here on
-    if (tid == 0) {
-        atomicExch(d.tw_count, 0);  // ready for the next launch
-        s_sfail = (atomicAdd(&d.tw_fail[0], 0) | atomicAdd(&d.tw_fail[1], 0)) ? 1 : 0;
-    }
-    __syncthreads();
     if (!s_sfail) {
     double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
     band_lds<BW>(lds, d.ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
