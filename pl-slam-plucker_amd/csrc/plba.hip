@@ -527,7 +527,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.huber_ln = g->huber_ln;
     d.tau = ctx->opts.tau;
     d.n_lin_blocks = blocks_for(E);
-    d.n_lm_blocks = blocks_for(n_lm);
+    d.n_lm_blocks = blocks_for(n_lm, kLmBlock);
     d.n_kf_blocks = blocks_for(n_kf);
 
     std::vector<double> T((size_t)n_kf * 12), X((size_t)n_lm * 4, 0.0);
@@ -712,7 +712,7 @@ int launch_step(plba_ctx *ctx) {
     const int nv = std::max(std::max(d.n_lm, d.n_kf), 1);
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kPoseNT), 0, s, d));
-    if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+    if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kLmBlock), 0, s, d));
     if (d.sharded) {
         LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kBlock), 0, s, d));
         COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 42 + 2 + d.nranks);
@@ -735,7 +735,7 @@ int launch_step(plba_ctx *ctx) {
     // the factorisation kernels end with the pose update; without free poses it runs alone
     if (d.n == 0 && d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(1), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) {
-        LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kBlock), 0, s, d));
+        LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kLmBlock), 0, s, d));
         LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }
     if (d.sharded) {

@@ -34,6 +34,7 @@
 namespace plba {
 
 constexpr int kBlock = 256;
+constexpr int kLmBlock = 64;  // landmark-parallel kernels: 24k landmarks at C3 -> 375 workgroups, not 94
 constexpr int kChunk = 128;  // Schur triples per assembly wave (2 per lane)
 constexpr int kTraceCap = 64;
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
@@ -347,10 +348,10 @@ __global__ __launch_bounds__(kPoseNT) void k_pose_reduce(Dev d) {
 // packed lower-triangular index for 4x4 symmetric
 __device__ __forceinline__ constexpr int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
-__global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
+__global__ __launch_bounds__(kLmBlock) void k_landmark_reduce(Dev d) {
     ITER_GUARD
-    __shared__ double sh[kBlock / 64];
-    const int l = blockIdx.x * kBlock + threadIdx.x;
+    __shared__ double sh[kLmBlock / 64];
+    const int l = blockIdx.x * kLmBlock + threadIdx.x;
     const bool sw = d.ctrl->switch_pending;
     double mx = 0.0;
     bool any = false;
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(kBlock) void k_landmark_reduce(Dev d) {
         for (int k = 0; k < 4; ++k) d.bl[(size_t)l * 4 + k] = b[k];
         mx = fmax(fmax(fabs(H[pk(0, 0)]), fabs(H[pk(1, 1)])), fmax(fabs(H[pk(2, 2)]), fabs(H[pk(3, 3)])));
     }
-    double m = block_max<kBlock>(mx, sh);
+    double m = block_max<kLmBlock>(mx, sh);
     const int anyb = __syncthreads_or(any ? 1 : 0);
     if (threadIdx.x == 0) {
         d.part_max[d.nf + blockIdx.x] = m;
@@ -1451,10 +1452,10 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
     d.q[(size_t)e * 2 + 1] = q1;
 }
 // per landmark: x_l = L⁻ᵀ L⁻¹ (b_l - Σ u_e), oplus into the trial state, scale partial
-__global__ __launch_bounds__(kBlock) void k_lm_solve(Dev d) {
+__global__ __launch_bounds__(kLmBlock) void k_lm_solve(Dev d) {
     TRIAL_GUARD
-    __shared__ double sh[kBlock / 64];
-    const int l = blockIdx.x * kBlock + threadIdx.x;
+    __shared__ double sh[kLmBlock / 64];
+    const int l = blockIdx.x * kLmBlock + threadIdx.x;
     double sc = 0.0;
     if (l < d.n_lm) {
         const double *Xc = Xcur(d) + (size_t)l * 4;
@@ -1530,7 +1531,7 @@ __global__ __launch_bounds__(kBlock) void k_lm_solve(Dev d) {
             for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
         }
     }
-    const double s2 = block_sum<kBlock>(sc, sh);
+    const double s2 = block_sum<kLmBlock>(sc, sh);
     if (threadIdx.x == 0) d.part_lms[blockIdx.x] = s2;
 }
 // per edge: χ² at the trial state (last-evaluated semantics), robust partial sums
