@@ -163,7 +163,9 @@ def main():
         alg = kernel_bytes(g, name, info)
         achieved = alg / (avg_ms * 1e-3) / 1e9
         # rocprofv3 names the banded factorisation by its template (k_rcs_factor_band<BW>)
-        prof_name = "k_rcs_factor_band" if name == "k_rcs_factor" and info.get("banded") else name
+        prof_name = name
+        if name == "k_rcs_factor" and info.get("banded"):
+            prof_name = "k_rcs_factor_twisted" if info.get("twisted") else "k_rcs_factor_band"
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
         traffic = None
         if os.path.exists(pmc_path):
@@ -217,7 +219,9 @@ def main():
                 "alg_bytes_per_launch": alg,
                 "avg_launch_us": avg_ms * 1e3,
                 "launches_per_lba": nl,
-                "note": "latency-bound single-workgroup banded LDLᵀ; see DESIGN.md §4",
+                "note": ("latency-bound banded LDLᵀ of the reduced camera system (a serial chain of 6x6 "
+                         "block pivots, two-sided on 2 workgroups) + pose update; bytes/launch are tiny by "
+                         "nature — see DESIGN.md §4"),
             },
             "iteration_roofline": {
                 "alg_bytes_per_iter": iter_bytes,

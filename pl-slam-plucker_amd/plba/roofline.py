@@ -39,25 +39,26 @@ def kernel_bytes(g: Graph, name: str, st: dict) -> float:
         return Ef * (I + 14 * F) + nf * (36 + 6 + 1) * F
     if name == "k_landmark_reduce":
         return E * (8 + 2) * F + n_lm * (I + (10 + 4) * F)
-    if name == "k_lm_chol":
-        return n_lm * (10 + 4 + 10 + 4) * F
     if name == "k_edge_schur":
+        # per edge: landmark index, B (8) in; Z (8), q (2) out; per landmark Hll (10) + b_l (4) once
         return E * (I + 8 * F + 10 * F) + n_lm * (10 + 4) * F
     if name == "k_rcs_chunk":
         # every edge's A (12) and Z (8), q (2) read once; the triple list; 42 partials per chunk
         return E * (12 + 8 + 2) * F + T * 2 * I + nch * 42 * F
     if name == "k_rcs_finalize":
         return nch * 42 * F + nf * (36 + 6) * F + nblk * blk + nf * 6 * F
-    if name in ("k_rcs_factor", "k_rcs_factor_band"):
-        # band in (nf·(bw+1) blocks) + b_s; L band, S⁻¹, z, x_p out
-        return nf * (bw + 1) * blk + nf * 6 * F + nf * bw * blk + nf * (36 + 6 + 6) * F
+    if name in ("k_rcs_factor", "k_rcs_factor_band", "k_rcs_factor_twisted"):
+        # band in (nf·(bw+1) blocks) + b_s; L band, S⁻¹, z, x_p out; then the pose update:
+        # current poses in, trial poses out, b_p in
+        return (nf * (bw + 1) * blk + nf * 6 * F + nf * bw * blk + nf * (36 + 6 + 6) * F
+                + g.n_kf * (12 + 12) * F + nf * 6 * F)
     if name == "k_pose_update":
         return g.n_kf * (12 + 12) * F + nf * 12 * F
-    if name == "k_edge_backsub":
-        return Ef * (I + (12 + 8) * F) + nf * 6 * F + E * 4 * F
     if name == "k_lm_solve":
-        return n_lm * (4 + 4 + 10 + 4 + 4) * F + n_lm * I + E * 4 * F + g.n_ln * 6 * F
+        # per landmark: X (4), b_l (4), Hll (10) in, X_trial (4), x_l (4) out; per free edge the
+        # back-substitution reads A (12) and B (8); x_p once
+        return n_lm * (4 + 4 + 10 + 4 + 4) * F + n_lm * I + Ef * (I + (12 + 8) * F) + nf * 6 * F
     if name == "k_edge_eval":
         rd = Ep * (2 * I + 2 * F + F + 1) + El * (2 * I + 4 * F + F + 1)
-        return rd + g.n_kf * 12 * F + g.n_pt * 3 * F + g.n_ln * 6 * F + E * F
+        return rd + g.n_kf * 12 * F + g.n_pt * 3 * F + g.n_ln * 4 * F + E * F
     return 0.0
