@@ -40,11 +40,11 @@ namespace plba {
     } while (0)
 
 enum KernelId {
-    K_LINEARIZE, K_POSE_REDUCE, K_LM_REDUCE, K_ITER_INIT, K_ESCHUR, K_MEMSET, K_ASSEMBLE, K_FINALIZE, K_FACTOR,
+    K_LINEARIZE, K_REDUCE, K_ITER_INIT, K_ESCHUR, K_MEMSET, K_ASSEMBLE, K_FINALIZE, K_FACTOR,
     K_POSE_UPDATE, K_LM_UPDATE, K_EVAL, K_DECIDE, K_COUNT
 };
 static const char *kKernelNames[K_COUNT] = {
-    "k_linearize", "k_pose_reduce", "k_landmark_reduce", "k_iter_init", "k_edge_schur", "memset_rcs",
+    "k_linearize", "k_iter_reduce", "k_iter_init", "k_edge_schur", "memset_rcs",
     "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_lm_solve", "k_edge_eval", "k_decide"};
 
 }  // namespace plba
@@ -616,6 +616,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_chi2, d.n_lin_blocks);
     ALLOC(d.part_any, d.n_lm_blocks);
     ALLOC(d.part_max, nf + d.n_lm_blocks);
+    ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * 27);
     ALLOC(d.part_lm, std::max(d.n_lin_blocks, d.n_lm_blocks));
     ALLOC(d.Xplk, (size_t)n_lm * 6);
     ALLOC(d.part_lms, d.n_lm_blocks);
@@ -711,13 +712,15 @@ int launch_step(plba_ctx *ctx) {
     hipStream_t s = ctx->stream;
     const int nv = std::max(std::max(d.n_lm, d.n_kf), 1);
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
-    if (d.nf > 0) LAUNCH(K_POSE_REDUCE, hipLaunchKernelGGL(k_pose_reduce, dim3(d.nf), dim3(kPoseNT), 0, s, d));
-    if (d.n_lm > 0) LAUNCH(K_LM_REDUCE, hipLaunchKernelGGL(k_landmark_reduce, dim3(d.n_lm_blocks), dim3(kLmBlock), 0, s, d));
+    if (d.nf > 0 || d.n_lm > 0) {
+        const int nred = kPoseParts * d.nf + (d.n_lm > 0 ? d.n_lm_blocks : 0);
+        LAUNCH(K_REDUCE, hipLaunchKernelGGL(k_iter_reduce, dim3(nred), dim3(kLmBlock), 0, s, d));
+    }
     if (d.sharded) {
-        LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kBlock), 0, s, d));
+        LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kInitNT), 0, s, d));
         COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 42 + 2 + d.nranks);
     }
-    LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kBlock), 0, s, d));
+    LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kInitNT), 0, s, d));
     if (d.n_lm > 0) {
         LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }

@@ -3,19 +3,22 @@
 // Per LM outer iteration (OptimizationAlgorithmLevenberg::solve):
 //   k_linearize        edge-parallel: error, χ², Huber weight, weighted Jacobians
 //                      (computeActiveErrors + linearizeOplus + constructQuadraticForm, A5/A6/A9/A10)
-//   k_pose_reduce      pose-parallel deterministic segmented sum: Hpp, b_p
-//   k_landmark_reduce  landmark-parallel: Hll, b_l; max|diag| partials
-//   k_iter_init        χ²_cur, λ init (τ·max|H_jj|, iteration 0)
+//   k_iter_reduce      one launch, two roles: pose-parallel partial sums of Hpp, b_p
+//                      (kPoseParts workgroups per pose) and landmark-parallel Hll, b_l,
+//                      max|diag| partials
+//   k_iter_init        Hpp, b_p from the pose parts, χ²_cur, λ init (τ·max|H_jj|, iteration 0)
 // Stage switch (initializeOptimization): folded into the iteration kernels of the first step
-// of a stage — k_linearize classifies and activates edges, k_landmark_reduce activates
+// of a stage — k_linearize classifies and activates edges, k_iter_reduce activates
 // landmarks, k_iter_init advances the stage (or skips it when nothing is active).
 // Per damped trial (TRIAL_GUARD):
 //   k_edge_schur       edge-parallel: (Hll+λI) = LLᵀ of its landmark, Z_e = B_e L⁻ᵀ, q_e = Z_e L⁻¹b_l
 //   k_rcs_chunk        one wave per chunk of <=128 (e1,e2) triples of one RCS block:
 //                      Σ A₁ᵀ(Z₁Z₂ᵀ)A₂ (and Σ A_eᵀq_e on diagonal blocks)
 //   k_rcs_finalize     per block entry: Hpp+λI − Σ chunks into the band (or dense) matrix, b_s
-//   k_rcs_factor_band<BW>  one workgroup: block-banded LDLᵀ + forward/backward solve
-//                      (LinearSolverEigen); k_rcs_factor is the dense-envelope fallback (bw>20)
+//   k_rcs_factor_twisted<BW>  two workgroups: two-sided block-banded LDLᵀ meeting at a
+//                      bw-block separator, forward/backward solve (LinearSolverEigen);
+//                      k_rcs_factor_band<BW> (one sweep) and the dense k_rcs_factor (bw>20)
+//                      are the fallbacks
 //                      ... each ending with the pose oplus of the free poses (pose_update_wg)
 //   k_lm_solve         landmark-parallel: x_l = L⁻ᵀL⁻¹(b_l − Σ_e B_eᵀA_e x_p), oplus, Σx(λx+b) partials
 //   k_edge_eval        edge-parallel: χ² at the trial state, robust partial sums
@@ -108,7 +111,7 @@ struct Dev {
     // reductions
     double *part_chi2;                  // [n_lin_blocks]
     int32_t *part_any;                  // [n_lm_blocks] block has an active landmark
-    double *part_max;                   // [nf + n_lm_blocks]
+    double *part_max;                   // [nf + n_lm_blocks] (landmark part from nf on)
     double *part_lm, *part_lms;         // [n_lin_blocks] trial χ² partials, [n_lm_blocks] scale partials
     double *Xplk;                       // [n_lm][6] trial Plücker of lines (xyz of points)
     double *part_ps;                    // [n_kf_blocks]
@@ -122,7 +125,8 @@ struct Dev {
     double *red_iter, *red_iter_loc;    // [nf*42 + 2 + nranks]: Hpp | b_p | χ² | active | lm max per rank
     double *red_rcs, *red_rcs_loc;      // [nblk*36 + nf*6]: Σ A₁ᵀZ₁Z₂ᵀA₂ per block | Σ A_eᵀq_e per pose
     double *red_dec, *red_dec_loc;      // [2]: trial χ² | landmark part of Σx(λx+b)
-    double *Hpp_w, *bp_w;               // where k_pose_reduce writes (== Hpp, bp unless sharded)
+    double *Hpp_w, *bp_w;               // where pose_combine writes (== Hpp, bp unless sharded)
+    double *pose_part;                  // [nf][kPoseParts][27] partial Σ AᵀA (upper), Σ Aᵀc
     int32_t *lm_gpos, *e_gpos;          // local landmark / edge -> whole-window position
     double *gat;                        // [n_lm_g*4 + 3*E_g] final gather buffer
     // two-sided banded factorisation (k_rcs_factor_twisted)
@@ -291,15 +295,25 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
     if (threadIdx.x == 0) d.part_chi2[blockIdx.x] = s;
 }
 
-// one workgroup per free pose: Hpp = Σ AᵀA, b_p = Σ Aᵀc (deterministic)
-constexpr int kPoseNT = 256;
-__global__ __launch_bounds__(kPoseNT) void k_pose_reduce(Dev d) {
-    ITER_GUARD
-    const int h = blockIdx.x;
+// The iteration's two reductions in ONE launch of 64-thread workgroups (they are independent
+// and each alone leaves most of the chip idle):
+//   workgroups [0, kPoseParts·nf): pose h, part j sums A_eᵀA_e and A_eᵀc_e over the pose's
+//     edges p ≡ 64j + lane (mod 64·kPoseParts) into pose_part[h][j][27]; the parts are added in
+//     j order by pose_combine (k_iter_init / k_iter_pack) — the same per-lane sets and order
+//     as one 256-thread workgroup per pose, so the sums are deterministic;
+//   workgroups [kPoseParts·nf, ...): 64 landmarks each, Hll = Σ B_eᵀB_e, b_l = Σ B_eᵀc_e
+//     (and, on a stage switch, the landmark activation).
+constexpr int kPoseParts = 4;
+constexpr int kInitNT = 1024;  // k_iter_init / k_iter_pack: one wide workgroup (the pose combine)
+
+// packed lower-triangular index for 4x4 symmetric
+__device__ __forceinline__ constexpr int pk(int r, int c) { return r * (r + 1) / 2 + c; }
+
+__device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-    for (int p = d.pe_off[h] + threadIdx.x; p < d.pe_off[h + 1]; p += kPoseNT) {
+    for (int p = d.pe_off[h] + part * 64 + threadIdx.x; p < d.pe_off[h + 1]; p += kPoseParts * 64) {
         const int e = d.pe_list[p];
         const double *A = d.A + (size_t)e * 12;
         const double *c = d.cvec + (size_t)e * 2;
@@ -315,43 +329,18 @@ __global__ __launch_bounds__(kPoseNT) void k_pose_reduce(Dev d) {
 #pragma unroll
         for (int r = 0; r < 6; ++r) acc[21 + r] += a0[r] * c0 + a1[r] * c1;
     }
-    __shared__ double sh27[kPoseNT / 64][27];
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = wave_sum(acc[k]);
-    if ((threadIdx.x & 63) == 0)
-#pragma unroll
-        for (int k = 0; k < 27; ++k) sh27[threadIdx.x >> 6][k] = acc[k];
-    __syncthreads();
-    double out[27];
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 27; ++k) {
-            double v = sh27[0][k];
-            for (int w = 1; w < kPoseNT / 64; ++w) v += sh27[w][k];
-            out[k] = v;
-        }
     if (threadIdx.x == 0) {
-        double *H = d.Hpp_w + (size_t)h * 36;
-        int idx = 0;
-        double mx = 0.0;
-        for (int r = 0; r < 6; ++r)
-            for (int cc = r; cc < 6; ++cc) {
-                H[r * 6 + cc] = out[idx];
-                H[cc * 6 + r] = out[idx];
-                if (r == cc) mx = fmax(mx, fabs(out[idx]));
-                ++idx;
-            }
-        for (int r = 0; r < 6; ++r) d.bp_w[(size_t)h * 6 + r] = out[21 + r];
-        d.part_max[h] = mx;
+        double *o = d.pose_part + ((size_t)h * kPoseParts + part) * 27;
+#pragma unroll
+        for (int k = 0; k < 27; ++k) o[k] = acc[k];
     }
 }
 
-// packed lower-triangular index for 4x4 symmetric
-__device__ __forceinline__ constexpr int pk(int r, int c) { return r * (r + 1) / 2 + c; }
-
-__global__ __launch_bounds__(kLmBlock) void k_landmark_reduce(Dev d) {
-    ITER_GUARD
+__device__ __forceinline__ void landmark_reduce(const Dev &d, int lb) {
     __shared__ double sh[kLmBlock / 64];
-    const int l = blockIdx.x * kLmBlock + threadIdx.x;
+    const int l = lb * kLmBlock + threadIdx.x;
     const bool sw = d.ctrl->switch_pending;
     double mx = 0.0;
     bool any = false;
@@ -389,56 +378,88 @@ __global__ __launch_bounds__(kLmBlock) void k_landmark_reduce(Dev d) {
     double m = block_max<kLmBlock>(mx, sh);
     const int anyb = __syncthreads_or(any ? 1 : 0);
     if (threadIdx.x == 0) {
-        d.part_max[d.nf + blockIdx.x] = m;
-        d.part_any[blockIdx.x] = anyb;
+        d.part_max[d.nf + lb] = m;
+        d.part_any[lb] = anyb;
     }
+}
+
+__global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
+    ITER_GUARD
+    const int b = blockIdx.x, np = kPoseParts * d.nf;
+    if (b < np) pose_partial(d, b / kPoseParts, b % kPoseParts);  // workgroup-uniform branch
+    else landmark_reduce(d, b - np);
+}
+
+// Hpp, b_p from the pose parts (added in part order); returns this thread's max |Hpp_jj|
+template <int NT>
+__device__ __forceinline__ double pose_combine(const Dev &d, double *H, double *bp) {
+    double m = 0.0;
+    for (int i = threadIdx.x; i < d.nf * 27; i += NT) {
+        const int h = i / 27, k = i % 27;
+        const double *src = d.pose_part + (size_t)h * kPoseParts * 27 + k;
+        double v = src[0];
+#pragma unroll
+        for (int j = 1; j < kPoseParts; ++j) v += src[j * 27];
+        if (k < 21) {
+            int r = 0, rem = k;
+            while (rem >= 6 - r) { rem -= 6 - r; ++r; }
+            const int cc = r + rem;
+            H[(size_t)h * 36 + r * 6 + cc] = v;
+            H[(size_t)h * 36 + cc * 6 + r] = v;
+            if (r == cc) m = fmax(m, fabs(v));
+        } else {
+            bp[(size_t)h * 6 + (k - 21)] = v;
+        }
+    }
+    return m;
 }
 
 // sharded windows: this rank's χ² and landmark max|diag| into the all-reduced iteration array
 // (Hpp and b_p already sit in it). The rank's max goes to its own slot: the sum over ranks of
 // one-hot slots is the list of maxima, reduced with max by k_iter_init.
-__global__ __launch_bounds__(kBlock) void k_iter_pack(Dev d) {
+__global__ __launch_bounds__(kInitNT) void k_iter_pack(Dev d) {
     ITER_GUARD
-    __shared__ double sh[kBlock / 64];
+    __shared__ double sh[kInitNT / 64];
+    (void)pose_combine<kInitNT>(d, d.Hpp_w, d.bp_w);
     double s = 0.0;
-    for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) s += d.part_chi2[i];
-    const double chi = block_sum<kBlock>(s, sh);
+    for (int i = threadIdx.x; i < d.n_lin_blocks; i += kInitNT) s += d.part_chi2[i];
+    const double chi = block_sum<kInitNT>(s, sh);
     double m = 0.0;
-    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[d.nf + i]);
-    const double mx = block_max<kBlock>(m, sh);
+    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) m = fmax(m, d.part_max[d.nf + i]);
+    const double mx = block_max<kInitNT>(m, sh);
     int any = 0;
-    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) any |= d.part_any[i];
+    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) any |= d.part_any[i];
     any = __syncthreads_or(any);
     double *o = d.red_iter_loc + (size_t)d.nf * 42;
     if (threadIdx.x == 0) {
         o[0] = chi;
         o[1] = any ? 1.0 : 0.0;
     }
-    for (int r = threadIdx.x; r < d.nranks; r += kBlock) o[2 + r] = r == d.rank ? mx : 0.0;
+    for (int r = threadIdx.x; r < d.nranks; r += kInitNT) o[2 + r] = r == d.rank ? mx : 0.0;
 }
 
-__global__ __launch_bounds__(kBlock) void k_iter_init(Dev d) {
+__global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
     ITER_GUARD
-    __shared__ double sh[kBlock / 64];
+    __shared__ double sh[kInitNT / 64];
     double chi, mx;
     bool any;
     if (d.sharded) {  // totals from the all-reduced iteration array
         const double *o = d.red_iter + (size_t)d.nf * 42;
         double m = 0.0;
-        for (int i = threadIdx.x; i < d.nf * 6; i += kBlock) m = fmax(m, fabs(d.Hpp[(i / 6) * 36 + (i % 6) * 7]));
-        for (int r = threadIdx.x; r < d.nranks; r += kBlock) m = fmax(m, o[2 + r]);
-        mx = block_max<kBlock>(m, sh);
+        for (int i = threadIdx.x; i < d.nf * 6; i += kInitNT) m = fmax(m, fabs(d.Hpp[(i / 6) * 36 + (i % 6) * 7]));
+        for (int r = threadIdx.x; r < d.nranks; r += kInitNT) m = fmax(m, o[2 + r]);
+        mx = block_max<kInitNT>(m, sh);
         chi = o[0];
         any = o[1] != 0.0;
     } else {
+        double m = pose_combine<kInitNT>(d, d.Hpp_w, d.bp_w);
         double s = 0.0;
-        for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) s += d.part_chi2[i];
-        chi = block_sum<kBlock>(s, sh);
-        double m = 0.0;
-        for (int i = threadIdx.x; i < d.nf + d.n_lm_blocks; i += kBlock) m = fmax(m, d.part_max[i]);
-        mx = block_max<kBlock>(m, sh);
+        for (int i = threadIdx.x; i < d.n_lin_blocks; i += kInitNT) s += d.part_chi2[i];
+        chi = block_sum<kInitNT>(s, sh);
+        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) m = fmax(m, d.part_max[d.nf + i]);
+        mx = block_max<kInitNT>(m, sh);
         int a = 0;
-        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) a |= d.part_any[i];
+        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) a |= d.part_any[i];
         any = __syncthreads_or(a) != 0;
     }
     if (threadIdx.x == 0) {

@@ -35,10 +35,14 @@ def kernel_bytes(g: Graph, name: str, st: dict) -> float:
         # write: A (12), c (2), B (8), χ² (1) per edge
         rd = Ep * (2 * I + 2 * F + F + 1 + I) + El * (2 * I + 4 * F + F + 1 + I) + state_bytes(g)
         return rd + E * (12 + 2 + 8 + 1) * F
-    if name == "k_pose_reduce":
-        return Ef * (I + 14 * F) + nf * (36 + 6 + 1) * F
-    if name == "k_landmark_reduce":
-        return E * (8 + 2) * F + n_lm * (I + (10 + 4) * F)
+    if name == "k_iter_reduce":
+        # pose role: per free edge its index, A (12), c (2); 4 parts x 27 partial sums per pose
+        # landmark role: per edge B (8), c (2); per landmark offset, Hll (10) + b_l (4) out
+        return (Ef * (I + 14 * F) + nf * 4 * 27 * F
+                + E * (8 + 2) * F + n_lm * (I + (10 + 4) * F))
+    if name == "k_iter_init":
+        # the pose parts in, Hpp (36) + b_p (6) out
+        return nf * 4 * 27 * F + nf * (36 + 6) * F
     if name == "k_edge_schur":
         # per edge: landmark index, B (8) in; Z (8), q (2) out; per landmark Hll (10) + b_l (4) once
         return E * (I + 8 * F + 10 * F) + n_lm * (10 + 4) * F
