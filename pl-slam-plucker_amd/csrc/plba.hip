@@ -208,7 +208,7 @@ inline int band_ring(int bw, int nf) {
 }
 inline size_t band_lds_bytes(int bw, int nf) { return sizeof(double) * band_lds_doubles(bw, band_ring(bw, nf)); }
 inline size_t twisted_lds_bytes(int bw, int nf) {
-    return band_lds_bytes(bw, nf) + sizeof(double) * twisted_extra_doubles(bw);
+    return band_lds_bytes(bw, nf) + sizeof(double) * (twisted_extra_doubles(bw) + (size_t)nf * 6);  // + x_p staging
 }
 inline void launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};

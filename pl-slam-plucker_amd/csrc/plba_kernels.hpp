@@ -1102,10 +1102,13 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
 // in registers): once x_i is final, its 6 values are read from the owning lanes with
 // v_readlane and every window row j = i-w applies z_j -= L_{i,j}ᵀ x_i at once. The chain per
 // step is one readlane batch + one 6-term dot product; no LDS round trips.
-template <int BW>
+// LX: x rows go to LDS (the caller copies them out) — a global store in the loop would make
+// the compiler's vmcnt waits (loads and stores share the counter) drain the L prefetches.
+template <int BW, bool LX = false>
 __device__ __forceinline__ void band_backward_rl(const double *Lband, const double *zb, int nsteps, int nrows,
                                                  const double *xsep, double *xp, bool reversed, int nf, int lane) {
     constexpr int W = BW + 1, kPipe = 4;
+    if (nsteps <= 0) return;
     const int G = lane / 6, r = lane % 6;      // lane group G holds the window row j ≡ G (mod BW)
     const bool act = lane < BW * 6;
     const int top = xsep ? min(nrows - 1, nsteps - 1 + BW) : nsteps - 1;
@@ -1115,25 +1118,33 @@ __device__ __forceinline__ void band_backward_rl(const double *Lband, const doub
         int j = top - ((top - G) % BW + BW) % BW;  // the row of this group in [top-BW+1, top]
         if (j >= 0) zv = j >= nsteps ? (xsep ? xsep[(j - nsteps) * 6 + r] : 0.0) : zb[(size_t)j * 6 + r];
     }
+    // Load cursor: row li's L block for this lane's window row li - wl, wl = ((li-G-1) mod BW)+1,
+    // stepped incrementally (wl cycles BW..1 as li decreases). Loads are unconditional from
+    // clamped in-range addresses and masked afterwards, so the loop carries no branches.
+    int li = top, wl = ((top - G - 1) % BW + BW) % BW + 1;
     double Lr[kPipe][6], zr[kPipe];
-    auto load_step = [&](int i, double (&dst)[6], double &z) {
-        // row i's L block for this lane's window row j = i - w, and z_{i-BW} for the group that
-        // takes row i-BW at step i
-        const int w = ((i - G - 1) % BW + BW) % BW + 1;
-        const bool ok = act && i >= 0 && i - w >= 0 && i - w < nsteps;
-        const double *L = Lband + ((size_t)max(i, 0) * W + w) * 36;
+    bool lok[kPipe], zok[kPipe];               // masks applied when the values are consumed, so
+    auto load_step = [&](double (&dst)[6], double &z, bool &okL, bool &okZ) {  // no load is waited on early
+        const int jl = li - wl;
+        okL = act && li >= 0 && jl >= 0 && jl < nsteps;
+        const int base = (max(li, 0) * W + wl) * 36 + r;
 #pragma unroll
-        for (int m = 0; m < 6; ++m) dst[m] = ok ? L[m * 6 + r] : 0.0;
-        z = (act && i - BW >= 0 && i - BW < nsteps) ? zb[(size_t)(i - BW) * 6 + r] : 0.0;
+        for (int m = 0; m < 6; ++m) dst[m] = Lband[base + m * 6];
+        const int iz = li - BW;
+        z = zb[min(max(iz, 0), nsteps - 1) * 6 + r];
+        okZ = act && iz >= 0 && iz < nsteps;
+        --li;
+        wl = wl == 1 ? BW : wl - 1;
     };
 #pragma unroll
-    for (int u = 0; u < kPipe; ++u) load_step(top - u, Lr[u], zr[u]);
+    for (int u = 0; u < kPipe; ++u) load_step(Lr[u], zr[u], lok[u], zok[u]);
+    int gi = top % BW;                          // group holding row i (final), uniform
+    // whole kPipe batches (trailing steps with i < 0 are masked no-ops): no exits inside the
+    // unrolled body, so the compiler can count the prefetches in flight exactly
     for (int ib = top; ib >= 0; ib -= kPipe) {
 #pragma unroll
         for (int u = 0; u < kPipe; ++u) {
             const int i = ib - u;
-            if (i < 0) break;
-            const int gi = i % BW;             // group holding row i (final)
             double x[6];
 #pragma unroll
             for (int m = 0; m < 6; ++m) {
@@ -1142,16 +1153,21 @@ __device__ __forceinline__ void band_backward_rl(const double *Lband, const doub
                 const int hi = __builtin_amdgcn_readlane(__double2hiint(zv), src);
                 x[m] = __hiloint2double(hi, lo);
             }
-            if (G == gi && act) {
-                if (i < nsteps) xp[(size_t)(reversed ? nf - 1 - i : i) * 6 + r] = zv;
-                zv = zr[u];                    // this group now holds row i-BW
+            const bool mine = act && G == gi && i >= 0;  // this group holds the final row i
+            if (mine && i < nsteps) {
+                const int row = reversed ? nf - 1 - i : i;
+                if constexpr (LX) ((__attribute__((address_space(3))) double *)xp)[row * 6 + r] = zv;
+                else xp[(size_t)row * 6 + r] = zv;
             }
-            // z_j -= L_{i,j}ᵀ x_i for the window rows j < nsteps (Lr is zero elsewhere)
+            // z_j -= L_{i,j}ᵀ x_i for the window rows j < nsteps (masked to zero elsewhere);
+            // the group that held row i takes row i-BW
             double acc = 0.0;
 #pragma unroll
             for (int m = 0; m < 6; ++m) acc = fma(Lr[u][m], x[m], acc);
-            zv -= acc;
-            load_step(i - kPipe, Lr[u], zr[u]);
+            const double znew = zok[u] ? zr[u] : 0.0;
+            zv = (mine ? znew : zv) - (lok[u] ? acc : 0.0);
+            load_step(Lr[u], zr[u], lok[u], zok[u]);
+            gi = gi == 0 ? BW - 1 : gi - 1;
         }
     }
 }
@@ -1290,6 +1306,7 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(Dev &d) {
     band_lds<BW>(lds, d.ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
     double *xr1 = lds + band_lds_doubles(BW, d.ring), *part1 = xr1 + W * 6;
     double *Ms = part1 + W * 6, *fcol = Ms + (size_t)NS * LD;
+    double *xl = lds + band_lds_doubles(BW, d.ring) + twisted_extra_doubles(BW);  // [nf][6] x_p staging
     // ---- separator system S_sep (lower block (i,j), i >= j, w = i-j) and its right-hand side
     const double *W0 = d.tw_sep, *W1 = d.tw_sep + sep_stride;
     for (int t = tid; t < NS * NS; t += NT) {
@@ -1361,19 +1378,21 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(Dev &d) {
 #pragma unroll
         for (int q = 0; q < 6; ++q) x = fma(Kp[P * 36 + a_ * 6 + q], Ms[(size_t)(P * 6 + q) * LD + NS], x);
         xs0[t] = x;
-        d.xp[(size_t)m * 6 + t] = x;
+        xl[(size_t)m * 6 + t] = x;
     }
     __syncthreads();
     double *xsr = Ms;  // reversed-order copy (Ms is no longer needed)
     for (int t = tid; t < NS; t += NT) xsr[t] = xs0[(BW - 1 - t / 6) * 6 + t % 6];
     __syncthreads();
     if constexpr (BW * 6 <= 64) {
-        if (tid < 64) band_backward_rl<BW>(d.Lband, d.zb, m, d.nf, xs0, d.xp, false, d.nf, tid);
-        else if (tid < 128) band_backward_rl<BW>(d.Lband2, d.zb2, n1, d.nf, xsr, d.xp, true, d.nf, tid - 64);
+        if (tid < 64) band_backward_rl<BW, true>(d.Lband, d.zb, m, d.nf, xs0, xl, false, d.nf, tid);
+        else if (tid < 128) band_backward_rl<BW, true>(d.Lband2, d.zb2, n1, d.nf, xsr, xl, true, d.nf, tid - 64);
     } else {
-        if (tid < 64) band_backward<BW>(d.Lband, d.zb, m, d.nf, xs0, d.xp, false, d.nf, xr, part, tid);
-        else if (tid < 128) band_backward<BW>(d.Lband2, d.zb2, n1, d.nf, xsr, d.xp, true, d.nf, xr1, part1, tid - 64);
+        if (tid < 64) band_backward<BW>(d.Lband, d.zb, m, d.nf, xs0, xl, false, d.nf, xr, part, tid);
+        else if (tid < 128) band_backward<BW>(d.Lband2, d.zb2, n1, d.nf, xsr, xl, true, d.nf, xr1, part1, tid - 64);
     }
+    __syncthreads();
+    for (int t = tid; t < d.nf * 6; t += NT) d.xp[t] = xl[t];
 #ifdef PLBA_STAMPS
     if (tid == 0) TW_MARK(3, __builtin_readcyclecounter() - tw_t2);
     if (tid == 0) TW_MARK(4, 1);
