@@ -528,6 +528,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.tau = ctx->opts.tau;
     d.n_lin_blocks = blocks_for(E);
     d.n_lm_blocks = blocks_for(n_lm, kLmBlock);
+    d.n_lms_blocks = blocks_for(n_lm * kLmLanes, kLmsNT);
     d.n_kf_blocks = blocks_for(n_kf);
 
     std::vector<double> T((size_t)n_kf * 12), X((size_t)n_lm * 4, 0.0);
@@ -619,7 +620,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * 27);
     ALLOC(d.part_lm, std::max(d.n_lin_blocks, d.n_lm_blocks));
     ALLOC(d.Xplk, (size_t)n_lm * 6);
-    ALLOC(d.part_lms, d.n_lm_blocks);
+    ALLOC(d.part_lms, d.n_lms_blocks);
     ALLOC(d.part_ps, d.n_kf_blocks);
     ALLOC(d.ctrl, 1);
     ALLOC(d.trace, kTraceCap);
@@ -738,7 +739,7 @@ int launch_step(plba_ctx *ctx) {
     // the factorisation kernels end with the pose update; without free poses it runs alone
     if (d.n == 0 && d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(1), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) {
-        LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lm_blocks), dim3(kLmBlock), 0, s, d));
+        LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lms_blocks), dim3(kLmsNT), 0, s, d));
         LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }
     if (d.sharded) {

@@ -67,6 +67,7 @@ struct Ctrl {
 struct Dev {
     int32_t n_kf, n_pt, n_ln, n_lm, Ep, El, E, nf, n;
     int32_t corrected, n_lin_blocks, n_lm_blocks, n_kf_blocks, nblk, ntiles;
+    int32_t n_lms_blocks;               // k_lm_solve workgroups (kLmLanes lanes per landmark)
     Cam cam;
     double huber_pt, huber_ln, tau;
     // state
@@ -1492,39 +1493,66 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
     d.q[(size_t)e * 2 + 1] = q1;
 }
 // per landmark: x_l = L⁻ᵀ L⁻¹ (b_l - Σ u_e), oplus into the trial state, scale partial
-__global__ __launch_bounds__(kLmBlock) void k_lm_solve(Dev d) {
+// quad (4-lane) DPP exchanges: xor 1 = quad_perm [1,0,3,2], xor 2 = quad_perm [2,3,0,1]
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// sum over the 4 lanes of a quad, identical in all four (a+b == b+a bitwise)
+__device__ __forceinline__ double quad_sum(double v) {
+    v += dpp_f64<0xB1>(v);
+    return v + dpp_f64<0x4E>(v);
+}
+
+// kLmLanes lanes per landmark: lane q walks edges q, q+4, ... of the landmark's CSR range for
+// the back-substitution sum, the quad adds the partials (DPP, fixed order), and every lane of
+// the quad then solves the 3x3/4x4 system redundantly; lane q writes component q.
+constexpr int kLmLanes = 4;
+constexpr int kLmsNT = 256;  // k_lm_solve workgroup: 64 landmarks
+__global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
     TRIAL_GUARD
-    __shared__ double sh[kLmBlock / 64];
-    const int l = blockIdx.x * kLmBlock + threadIdx.x;
+    __shared__ double sh[kLmsNT / 64];
+    const int gt = blockIdx.x * kLmsNT + threadIdx.x;
+    const int l = gt / kLmLanes, q = gt % kLmLanes;   // a quad never straddles a wave
+    const bool live = l < d.n_lm;
+    const bool act = live && d.lm_active[l] != 0;
+    const bool solve = d.ctrl->solve_ok != 0;
+    // r = b_l − Σ_e Hpl_eᵀ x_p,  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)  (edges of a fixed pose: 0)
+    double u[4] = {0, 0, 0, 0};
+    if (act && solve) {
+        for (int e = d.lm_off[l] + q; e < d.lm_off[l + 1]; e += kLmLanes) {
+            const int h = d.e_hidx[e];
+            if (h < 0) continue;
+            const double *A = d.A + (size_t)e * 12;
+            const double *Bm = d.B + (size_t)e * 8;
+            double ax0 = 0, ax1 = 0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const double xk = d.xp[6 * h + k];
+                ax0 += A[k] * xk;
+                ax1 += A[6 + k] * xk;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) u[i] += Bm[i] * ax0 + Bm[4 + i] * ax1;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = quad_sum(u[i]);  // all lanes: DPP reads the whole quad
     double sc = 0.0;
-    if (l < d.n_lm) {
+    if (live) {
         const double *Xc = Xcur(d) + (size_t)l * 4;
         double *Xt = Xtrial(d) + (size_t)l * 4;
-        if (d.lm_active[l]) {
+        if (act) {
             const bool pt = is_point_lm(d, l);
             const int DIM = pt ? 3 : 4;
             const double lam = d.ctrl->lambda;
             double x[4] = {0, 0, 0, 0};
-            if (d.ctrl->solve_ok) {
-                // r = b_l − Σ_e Hpl_eᵀ x_p,  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)  (edges of a fixed pose: 0)
+            if (solve) {
                 double r[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) r[i] = d.bl[(size_t)l * 4 + i];
-                for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
-                    const int h = d.e_hidx[e];
-                    if (h < 0) continue;
-                    const double *A = d.A + (size_t)e * 12;
-                    const double *Bm = d.B + (size_t)e * 8;
-                    double ax0 = 0, ax1 = 0;
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) {
-                        const double xk = d.xp[6 * h + k];
-                        ax0 += A[k] * xk;
-                        ax1 += A[6 + k] * xk;
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) r[i] -= Bm[i] * ax0 + Bm[4 + i] * ax1;
-                }
+                for (int i = 0; i < 4; ++i) r[i] = d.bl[(size_t)l * 4 + i] - u[i];
                 double L[10], gl[4], y[4] = {0, 0, 0, 0};
                 lm_chol(d, l, lam, L, gl);
 #pragma unroll
@@ -1544,15 +1572,12 @@ __global__ __launch_bounds__(kLmBlock) void k_lm_solve(Dev d) {
                             if (p < DIM) t -= L[pk(p, i)] * x[p];
                         x[i] = t / L[pk(i, i)];
                     }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) d.xl[(size_t)l * 4 + i] = x[i];
+                d.xl[(size_t)l * 4 + q] = x[q];
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) x[i] = d.xl[(size_t)l * 4 + i];
             }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (i < DIM) sc += x[i] * (lam * x[i] + d.bl[(size_t)l * 4 + i]);
+            if (q < DIM) sc = x[q] * (lam * x[q] + d.bl[(size_t)l * 4 + q]);
             double X[4];
             if (pt) {
                 X[0] = Xc[0] + x[0]; X[1] = Xc[1] + x[1]; X[2] = Xc[2] + x[2]; X[3] = 0.0;
@@ -1561,17 +1586,17 @@ __global__ __launch_bounds__(kLmBlock) void k_lm_solve(Dev d) {
                 orth_oplus(in, x, X);
                 double Lp[6];
                 orth_to_pluker(X, Lp);
-#pragma unroll
-                for (int k = 0; k < 6; ++k) d.Xplk[(size_t)l * 6 + k] = Lp[k];
+                if (q < 3) {
+                    d.Xplk[(size_t)l * 6 + 2 * q] = Lp[2 * q];
+                    d.Xplk[(size_t)l * 6 + 2 * q + 1] = Lp[2 * q + 1];
+                }
             }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Xt[i] = X[i];
+            Xt[q] = X[q];
         } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
+            Xt[q] = Xc[q];
         }
     }
-    const double s2 = block_sum<kLmBlock>(sc, sh);
+    const double s2 = block_sum<kLmsNT>(sc, sh);
     if (threadIdx.x == 0) d.part_lms[blockIdx.x] = s2;
 }
 // per edge: χ² at the trial state (last-evaluated semantics), robust partial sums
@@ -1610,7 +1635,7 @@ __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
     __shared__ double sh[kBlock / 64];
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
-    for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) b += d.part_lms[i];
+    for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) b += d.part_lms[i];
     const double ta = block_sum<kBlock>(a, sh);
     const double tb = block_sum<kBlock>(b, sh);
     if (threadIdx.x == 0) {
@@ -1626,7 +1651,7 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
     double a = 0.0, b = 0.0;
     if (!d.sharded) {
         for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
-        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kBlock) b += d.part_lms[i];
+        for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) b += d.part_lms[i];
     }
     for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];  // poses: replicated
     double tempChi0 = block_sum<kBlock>(a, sh);
