@@ -314,21 +314,36 @@ __device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-    for (int p = d.pe_off[h] + part * 64 + threadIdx.x; p < d.pe_off[h + 1]; p += kPoseParts * 64) {
-        const int e = d.pe_list[p];
-        const double *A = d.A + (size_t)e * 12;
-        const double *c = d.cvec + (size_t)e * 2;
-        double a0[6], a1[6];
+    // kU edges per pass with all their loads issued before the arithmetic (the per-thread
+    // chains are edge-index -> A/c misses; one edge at a time leaves them serialised)
+    constexpr int S = kPoseParts * 64, kU = 4;
+    const int pend = d.pe_off[h + 1];
+    for (int p0 = d.pe_off[h] + part * 64 + threadIdx.x; p0 < pend; p0 += kU * S) {
+        int ei[kU];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) { a0[k] = A[k]; a1[k] = A[6 + k]; }
-        const double c0 = c[0], c1 = c[1];
-        int idx = 0;
+        for (int j = 0; j < kU; ++j) ei[j] = p0 + j * S < pend ? d.pe_list[p0 + j * S] : -1;
+        double a[kU][12], cv[kU][2];
 #pragma unroll
-        for (int r = 0; r < 6; ++r)
+        for (int j = 0; j < kU; ++j) {
+            const int e = ei[j] < 0 ? ei[0] : ei[j];  // in-range address; masked below
+            const double *A = d.A + (size_t)e * 12;
 #pragma unroll
-            for (int cc = r; cc < 6; ++cc) acc[idx++] += a0[r] * a0[cc] + a1[r] * a1[cc];
+            for (int k = 0; k < 12; ++k) a[j][k] = A[k];
+            cv[j][0] = d.cvec[(size_t)e * 2];
+            cv[j][1] = d.cvec[(size_t)e * 2 + 1];
+        }
 #pragma unroll
-        for (int r = 0; r < 6; ++r) acc[21 + r] += a0[r] * c0 + a1[r] * c1;
+        for (int j = 0; j < kU; ++j) {
+            if (ei[j] < 0) break;
+            const double *a0 = a[j], *a1 = a[j] + 6;
+            int idx = 0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+#pragma unroll
+                for (int cc = r; cc < 6; ++cc) acc[idx++] += a0[r] * a0[cc] + a1[r] * a1[cc];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) acc[21 + r] += a0[r] * cv[j][0] + a1[r] * cv[j][1];
+        }
     }
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = wave_sum(acc[k]);
@@ -357,17 +372,27 @@ __device__ __forceinline__ void landmark_reduce(const Dev &d, int lb) {
         for (int k = 0; k < 10; ++k) H[k] = 0.0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) b[k] = 0.0;
-        for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
-            const double *B = d.B + (size_t)e * 8;
-            const double *c = d.cvec + (size_t)e * 2;
-            double b0[4], b1[4];
+        const int e1 = d.lm_off[l + 1];
+        for (int e0 = d.lm_off[l]; e0 < e1; e0 += 2) {  // two edges' loads in flight per pass
+            double bb[2][8], cc2[2][2];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) { b0[k] = B[k]; b1[k] = B[4 + k]; }
+            for (int j = 0; j < 2; ++j) {
+                const int e = e0 + j < e1 ? e0 + j : e0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+                for (int k = 0; k < 8; ++k) bb[j][k] = d.B[(size_t)e * 8 + k];
+                cc2[j][0] = d.cvec[(size_t)e * 2];
+                cc2[j][1] = d.cvec[(size_t)e * 2 + 1];
+            }
 #pragma unroll
-                for (int cc = 0; cc <= r; ++cc) H[pk(r, cc)] += b0[r] * b0[cc] + b1[r] * b1[cc];
-                b[r] += b0[r] * c[0] + b1[r] * c[1];
+            for (int j = 0; j < 2; ++j) {
+                if (e0 + j >= e1) break;
+                const double *b0 = bb[j], *b1 = bb[j] + 4;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                    for (int cc = 0; cc <= r; ++cc) H[pk(r, cc)] += b0[r] * b0[cc] + b1[r] * b1[cc];
+                    b[r] += b0[r] * cc2[j][0] + b1[r] * cc2[j][1];
+                }
             }
         }
 #pragma unroll
