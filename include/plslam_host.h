@@ -69,6 +69,8 @@ int plslam_line_add_observation(plslam_map *m, int32_t idx, const uint8_t *desc,
                                 double sigma2);
 /* the `local` flag of a keyframe (kind 0), point (1) or line (2). */
 int plslam_set_local(plslam_map *m, int32_t kind, int32_t idx, int32_t local);
+/* the `inlier` flag of a point (kind 1) or line (2). */
+int plslam_set_inlier(plslam_map *m, int32_t kind, int32_t idx, int32_t inlier);
 /* full_graph (n x n, row-major); map_points_kf_idx[kf] = lm[0..n) (creates the key, even empty) */
 int plslam_set_full_graph(plslam_map *m, int32_t n, const uint32_t *g);
 int plslam_get_full_graph(plslam_map *m, int32_t n, uint32_t *g);
@@ -77,6 +79,26 @@ int plslam_kf_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int3
 
 /* MapHandler::localBundleAdjustmentForPlukerWithG2O() */
 int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats);
+
+/* ---- the rest of the Plücker local-mapping step around the LBA ---- */
+/* SlamConfig::minLMObs / minLMCovGraph / minKFLocalMap (src/slamConfig.cpp:48,61-62; defaults
+ * 5 / 75 / 3) and MapHandler::max_kf_idx (include/mapHandler.h, src/mapHandler.cpp:135,173). */
+int plslam_set_params(plslam_map *m, int32_t min_lm_obs, int32_t min_lm_cov_graph, int32_t min_kf_local_map);
+int plslam_set_max_kf_idx(plslam_map *m, int32_t max_kf_idx);
+/* map_lines_kf_idx[kf] (include/mapHandler.h:149) */
+int plslam_kf_lines_idx_set(plslam_map *m, int32_t kf, const int32_t *lm, int32_t n);
+int plslam_kf_lines_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int32_t *n);
+/* MapHandler::formLocalMap(KeyFrame*) (src/mapHandler.cpp:1073-1137) */
+int plslam_form_local_map(plslam_map *m, int32_t kf_idx);
+/* MapHandler::removeBadMapLandmarksForPluker() (src/mapHandler.cpp:3816-3897); counts may be NULL */
+int plslam_remove_bad_landmarks_pluker(plslam_map *m, int32_t *n_pt_removed, int32_t *n_ln_removed);
+/* localMappingThread's USE_LINE_PLUKER body (src/mapHandler.cpp:1274-1279) after
+ * lookForCommonMatches (front-end matching, the caller's): formLocalMap(kf) -> LBA -> culling */
+int plslam_local_mapping_step(plslam_map *m, int32_t kf_idx, plslam_lba_stats *stats, int32_t *n_pt_removed,
+                              int32_t *n_ln_removed);
+/* 1 if map_points[idx] (kind 1) / map_lines[idx] (kind 2) / map_keyframes[idx] (kind 0) is
+ * non-NULL, else 0 */
+int plslam_exists(plslam_map *m, int32_t kind, int32_t idx, int32_t *exists);
 
 /* State readers (any pointer may be NULL). n_obs receives the observation count; the list
  * outputs are written up to `cap` entries. */

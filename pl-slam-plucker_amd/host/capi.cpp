@@ -120,6 +120,19 @@ int plslam_set_local(plslam_map *m, int32_t kind, int32_t idx, int32_t local) {
     }
 }
 
+int plslam_set_inlier(plslam_map *m, int32_t kind, int32_t idx, int32_t inlier) {
+    if (!m) return PLBA_E_INVALID;
+    if (kind == 1 && slot_ok(m->mh.map_points, idx)) {
+        m->mh.map_points[idx]->inlier = inlier != 0;
+        return PLBA_OK;
+    }
+    if (kind == 2 && slot_ok(m->mh.map_lines, idx)) {
+        m->mh.map_lines[idx]->inlier = inlier != 0;
+        return PLBA_OK;
+    }
+    return PLBA_E_INVALID;
+}
+
 int plslam_set_full_graph(plslam_map *m, int32_t n, const uint32_t *g) {
     if (!m || n < 0 || (n && !g)) return PLBA_E_INVALID;
     m->mh.full_graph.assign(n, std::vector<unsigned int>(n, 0));
@@ -153,11 +166,7 @@ int plslam_kf_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int3
     return PLBA_OK;
 }
 
-int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats) {
-    if (!m) return PLBA_E_INVALID;
-    LbaStats st;
-    const int rc = m->mh.localBundleAdjustmentForPlukerWithG2O(&st);
-    if (rc) return rc;
+static void copy_stats(const LbaStats &st, plslam_lba_stats *stats) {
     if (stats) {
         stats->n_free_kf = st.n_free_kf; stats->n_fixed_kf = st.n_fixed_kf;
         stats->n_pt = st.n_pt; stats->n_ln = st.n_ln; stats->n_ept = st.n_ept; stats->n_eln = st.n_eln;
@@ -168,7 +177,85 @@ int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats) {
         stats->chi2[0] = st.chi2[0]; stats->chi2[1] = st.chi2[1];
         stats->gather_ms = st.gather_ms; stats->solve_ms = st.solve_ms; stats->bookkeeping_ms = st.bookkeeping_ms;
     }
+}
+
+int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats) {
+    if (!m) return PLBA_E_INVALID;
+    LbaStats st;
+    const int rc = m->mh.localBundleAdjustmentForPlukerWithG2O(&st);
+    if (rc) return rc;
+    copy_stats(st, stats);
     return PLBA_OK;
+}
+
+int plslam_set_params(plslam_map *m, int32_t min_lm_obs, int32_t min_lm_cov_graph, int32_t min_kf_local_map) {
+    if (!m) return PLBA_E_INVALID;
+    m->mh.params.min_lm_obs = min_lm_obs;
+    m->mh.params.min_lm_cov_graph = min_lm_cov_graph;
+    m->mh.params.min_kf_local_map = min_kf_local_map;
+    return PLBA_OK;
+}
+
+int plslam_set_max_kf_idx(plslam_map *m, int32_t max_kf_idx) {
+    if (!m) return PLBA_E_INVALID;
+    m->mh.max_kf_idx = max_kf_idx;
+    return PLBA_OK;
+}
+
+int plslam_kf_lines_idx_set(plslam_map *m, int32_t kf, const int32_t *lm, int32_t n) {
+    if (!m || n < 0 || (n && !lm)) return PLBA_E_INVALID;
+    m->mh.map_lines_kf_idx[kf].assign(lm, lm + n);
+    return PLBA_OK;
+}
+
+int plslam_kf_lines_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int32_t *n) {
+    if (!m || !n) return PLBA_E_INVALID;
+    auto it = m->mh.map_lines_kf_idx.find(kf);
+    if (it == m->mh.map_lines_kf_idx.end()) {
+        *n = -1;
+        return PLBA_OK;
+    }
+    *n = (int32_t)it->second.size();
+    for (int i = 0; out && i < *n && i < cap; ++i) out[i] = it->second[i];
+    return PLBA_OK;
+}
+
+int plslam_form_local_map(plslam_map *m, int32_t kf_idx) {
+    if (!m) return PLBA_E_INVALID;
+    return m->mh.formLocalMap(kf_idx);
+}
+
+int plslam_remove_bad_landmarks_pluker(plslam_map *m, int32_t *n_pt_removed, int32_t *n_ln_removed) {
+    if (!m) return PLBA_E_INVALID;
+    CullStats cs;
+    const int rc = m->mh.removeBadMapLandmarksForPluker(&cs);
+    if (rc) return rc;
+    if (n_pt_removed) *n_pt_removed = cs.points_removed;
+    if (n_ln_removed) *n_ln_removed = cs.lines_removed;
+    return PLBA_OK;
+}
+
+int plslam_local_mapping_step(plslam_map *m, int32_t kf_idx, plslam_lba_stats *stats, int32_t *n_pt_removed,
+                              int32_t *n_ln_removed) {
+    if (!m) return PLBA_E_INVALID;
+    LbaStats st;
+    CullStats cs;
+    const int rc = m->mh.localMappingStep(kf_idx, &st, &cs);
+    if (rc) return rc;
+    copy_stats(st, stats);
+    if (n_pt_removed) *n_pt_removed = cs.points_removed;
+    if (n_ln_removed) *n_ln_removed = cs.lines_removed;
+    return PLBA_OK;
+}
+
+int plslam_exists(plslam_map *m, int32_t kind, int32_t idx, int32_t *exists) {
+    if (!m || !exists) return PLBA_E_INVALID;
+    switch (kind) {
+        case 0: *exists = slot_ok(m->mh.map_keyframes, idx); return PLBA_OK;
+        case 1: *exists = slot_ok(m->mh.map_points, idx); return PLBA_OK;
+        case 2: *exists = slot_ok(m->mh.map_lines, idx); return PLBA_OK;
+        default: return PLBA_E_INVALID;
+    }
 }
 
 int plslam_get_keyframe(plslam_map *m, int32_t kf_idx, double T_kf_w[16], int32_t *local, int32_t *pt_idx,

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 
 namespace plslam {
 
@@ -506,6 +507,149 @@ int MapHandler::localBundleAdjustmentForPlukerWithG2O(LbaStats *stats) {
     st.bookkeeping_ms = std::chrono::duration<double, std::milli>(t3 - t2).count();
     if (stats) *stats = st;
     return PLBA_OK;
+}
+
+// ----------------------------------------------------------------------------- local mapping
+// formLocalMap(KeyFrame*) (src/mapHandler.cpp:1073-1137). The reference dereferences
+// map_keyframes[i] and map_points[lm_idx] unchecked; a map on which it would crash is refused
+// here before any flag changes.
+int MapHandler::formLocalMap(int kf_idx) {
+    if (kf_idx < 0 || kf_idx >= (int)map_keyframes.size() || !map_keyframes[kf_idx]) {
+        setError("formLocalMap: no keyframe %d", kf_idx);
+        return PLBA_E_INVALID;
+    }
+    const int g_size = (int)full_graph.size() - 1;
+    auto in_window = [&](int i) {  // :1117
+        return full_graph[g_size][i] >= (unsigned)params.min_lm_cov_graph || std::abs(g_size - i) <= params.min_kf_local_map;
+    };
+    auto feats_ok = [&](const KeyFrame *k) {
+        for (int lm : k->stereo_frame.stereo_pt_idx)
+            if (lm < -1 || lm >= (int)map_points.size()) return false;
+        for (int lm : k->stereo_frame.stereo_ls_idx)
+            if (lm < -1 || lm >= (int)map_lines.size()) return false;
+        return true;
+    };
+    if (!feats_ok(map_keyframes[kf_idx])) {
+        setError("formLocalMap: keyframe %d has a feature idx outside the map", kf_idx);
+        return PLBA_E_INVALID;
+    }
+    for (int i = 0; i < g_size; ++i) {
+        if ((int)full_graph[g_size].size() <= i) {
+            setError("formLocalMap: full_graph row %d too short", g_size);
+            return PLBA_E_INVALID;
+        }
+        if (!in_window(i)) continue;
+        if (i >= (int)map_keyframes.size() || !map_keyframes[i] || !feats_ok(map_keyframes[i])) {
+            setError("formLocalMap: covisible keyframe %d missing or inconsistent", i);
+            return PLBA_E_INVALID;
+        }
+    }
+    // reset local KFs & LMs (:1076-1091)
+    for (auto *k : map_keyframes)
+        if (k) k->local = false;
+    for (auto *p : map_points)
+        if (p) p->local = false;
+    for (auto *l : map_lines)
+        if (l) l->local = false;
+    auto mark = [&](const KeyFrame *k) {
+        for (int lm : k->stereo_frame.stereo_pt_idx)
+            if (lm != -1 && map_points[lm]) map_points[lm]->local = true;
+        for (int lm : k->stereo_frame.stereo_ls_idx)
+            if (lm != -1 && map_lines[lm]) map_lines[lm]->local = true;
+    };
+    // the KF itself and its landmarks (:1094-1113)
+    map_keyframes[kf_idx]->local = true;
+    mark(map_keyframes[kf_idx]);
+    // covisible / recent keyframes from the last full_graph row (:1115-1135)
+    for (int i = 0; i < g_size; ++i)
+        if (in_window(i)) {
+            map_keyframes[i]->local = true;
+            mark(map_keyframes[i]);
+        }
+    return PLBA_OK;
+}
+
+// removeBadMapLandmarksForPluker (src/mapHandler.cpp:3816-3897). Candidates: non-local
+// landmarks whose first observing KF is more than 10 KFs old, that are outliers or have fewer
+// than min_lm_obs observations. The KF's feature idx is reset, the first matching entry of
+// map_points_kf_idx / map_lines_kf_idx is erased (`.at()`: a missing key is an error here,
+// checked before anything is removed) and the landmark is deleted (slot -> NULL).
+int MapHandler::removeBadMapLandmarksForPluker(CullStats *cs) {
+    CullStats st;
+    auto is_bad = [&](bool local, bool inlier, const std::vector<int> &kf_obs, size_t n_obs) {
+        return !local && max_kf_idx - kf_obs[0] > 10 && (!inlier || (int)n_obs < params.min_lm_obs);
+    };
+    auto check = [&](int kf_obs, const std::map<int, std::vector<int>> &kidx, const char *what, int idx) {
+        if (kf_obs < 0 || kf_obs >= (int)map_keyframes.size() || !map_keyframes[kf_obs]) {
+            setError("removeBadMapLandmarksForPluker: %s %d: no keyframe %d", what, idx, kf_obs);
+            return false;
+        }
+        if (!kidx.count(kf_obs)) {
+            setError("removeBadMapLandmarksForPluker: %s %d: %s_kf_idx.at(%d): no such key", what, idx, what, kf_obs);
+            return false;
+        }
+        return true;
+    };
+    for (auto *p : map_points)
+        if (p) {
+            if (p->kf_obs_list.empty()) {
+                setError("removeBadMapLandmarksForPluker: point %d has no observation", p->idx);
+                return PLBA_E_STATE;
+            }
+            if (is_bad(p->local, p->inlier, p->kf_obs_list, p->obs_list.size()) &&
+                !check(p->kf_obs_list[0], map_points_kf_idx, "map_points", p->idx))
+                return PLBA_E_STATE;
+        }
+    for (auto *l : map_lines)
+        if (l) {
+            if (l->kf_obs_list.empty()) {
+                setError("removeBadMapLandmarksForPluker: line %d has no observation", l->idx);
+                return PLBA_E_STATE;
+            }
+            if (is_bad(l->local, l->inlier, l->kf_obs_list, l->NDw_obs_list.size()) &&
+                !check(l->kf_obs_list[0], map_lines_kf_idx, "map_lines", l->idx))
+                return PLBA_E_STATE;
+        }
+    auto erase_first = [](std::vector<int> &v, int x) {
+        auto it = std::find(v.begin(), v.end(), x);
+        if (it != v.end()) v.erase(it);
+    };
+    for (auto *&p : map_points)
+        if (p && is_bad(p->local, p->inlier, p->kf_obs_list, p->obs_list.size())) {
+            const int kf_obs = p->kf_obs_list[0], lm_idx = p->idx;
+            for (int &f : map_keyframes[kf_obs]->stereo_frame.stereo_pt_idx)
+                if (f == lm_idx) {
+                    f = -1;
+                    break;
+                }
+            erase_first(map_points_kf_idx.at(kf_obs), lm_idx);
+            delete p;
+            p = nullptr;
+            st.points_removed++;
+        }
+    for (auto *&l : map_lines)
+        if (l && is_bad(l->local, l->inlier, l->kf_obs_list, l->NDw_obs_list.size())) {
+            const int kf_obs = l->kf_obs_list[0], lm_idx = l->idx;
+            for (int &f : map_keyframes[kf_obs]->stereo_frame.stereo_ls_idx)
+                if (f == lm_idx) {
+                    f = -1;
+                    break;
+                }
+            erase_first(map_lines_kf_idx.at(kf_obs), lm_idx);
+            delete l;
+            l = nullptr;
+            st.lines_removed++;
+        }
+    if (cs) *cs = st;
+    return PLBA_OK;
+}
+
+int MapHandler::localMappingStep(int kf_idx, LbaStats *stats, CullStats *cs) {
+    int rc = formLocalMap(kf_idx);  // :1274
+    if (rc) return rc;
+    rc = localBundleAdjustmentForPlukerWithG2O(stats);  // :1278
+    if (rc) return rc;
+    return removeBadMapLandmarksForPluker(cs);  // :1279
 }
 
 }  // namespace plslam

@@ -108,6 +108,17 @@ struct LbaStats {
 
 using SolveFn = int (*)(void *user, const plba_graph *g, plba_result *r);
 
+// The SlamConfig values the local-mapping step reads (src/slamConfig.cpp:48,61-62 defaults).
+struct SlamParams {
+    int min_lm_obs = 5;         // SlamConfig::minLMObs()
+    int min_lm_cov_graph = 75;  // SlamConfig::minLMCovGraph()
+    int min_kf_local_map = 3;   // SlamConfig::minKFLocalMap()
+};
+
+struct CullStats {
+    int points_removed = 0, lines_removed = 0;
+};
+
 // include/mapHandler.h:141-151 (the members the LBA uses)
 class MapHandler {
   public:
@@ -120,7 +131,21 @@ class MapHandler {
     std::vector<MapPoint *> map_points;
     std::vector<MapLine *> map_lines;
     std::map<int, std::vector<int>> map_points_kf_idx;
+    std::map<int, std::vector<int>> map_lines_kf_idx;
     std::vector<std::vector<unsigned int>> full_graph;
+    int max_kf_idx = 0;
+    SlamParams params;
+
+    // src/mapHandler.cpp:1073-1137: the local window around `kf` (covisibility >= min_lm_cov_graph
+    // landmarks or within min_kf_local_map keyframes of the newest), by the `local` flags.
+    int formLocalMap(int kf_idx);
+    // src/mapHandler.cpp:3816-3897: delete old non-local landmarks that are outliers or have
+    // fewer than min_lm_obs observations (slots become NULL).
+    int removeBadMapLandmarksForPluker(CullStats *cs = nullptr);
+    // The USE_LINE_PLUKER body of localMappingThread (src/mapHandler.cpp:1264-1280) after
+    // lookForCommonMatches (front-end descriptor matching, not part of this library):
+    // formLocalMap(kf) -> localBundleAdjustmentForPlukerWithG2O() -> removeBadMapLandmarksForPluker().
+    int localMappingStep(int kf_idx, LbaStats *stats = nullptr, CullStats *cs = nullptr);
 
     // src/mapHandler.cpp:5851. Returns PLBA_OK or a PLBA_E_* status (the reference exit(0)s
     // on an inconsistent map, :5894,5910,5998,6062; here the map is left untouched then).

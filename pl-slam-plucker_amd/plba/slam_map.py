@@ -62,6 +62,8 @@ class SlamMap:
     lines: List[Optional[Landmark]]
     map_points_kf_idx: Dict[int, List[int]]
     full_graph: np.ndarray        # (n_kf, n_kf) uint32
+    map_lines_kf_idx: Dict[int, List[int]] = dataclasses.field(default_factory=dict)
+    max_kf_idx: int = 0           # MapHandler::max_kf_idx (the newest KF)
 
     def copy(self) -> "SlamMap":
         import copy
@@ -147,11 +149,15 @@ def make_map(g: Graph, seed: int = 0, n_extra_kf: int = 2, n_extra_pt: int = 5, 
     for kf in kfs:
         kf.pt_idx.append(-1)
         rng.shuffle(kf.pt_idx)
-    # map_points_kf_idx: base KF -> landmarks (points and lines share it, as in the reference)
+    # map_points_kf_idx / map_lines_kf_idx: base KF -> its points / lines (the LBA's outlier
+    # pass looks lines up in map_points_kf_idx, src/mapHandler.cpp:6239-6251)
     kidx: Dict[int, List[int]] = {k: [] for k in range(n_kf)}
-    for lm in points + lines:
+    lidx: Dict[int, List[int]] = {k: [] for k in range(n_kf)}
+    for lm in points:
         if lm is not None:
             kidx[lm.kf_obs_list[0]].append(lm.idx)
+    for lm in lines:
+        lidx[lm.kf_obs_list[0]].append(lm.idx)
     fg = np.zeros((n_kf, n_kf), np.uint32)
     for lm in points + lines:
         if lm is not None:
@@ -160,7 +166,7 @@ def make_map(g: Graph, seed: int = 0, n_extra_kf: int = 2, n_extra_pt: int = 5, 
                     if a != b:
                         fg[a, b] += 1
     fg += 3   # so a few decrements never wrap
-    return SlamMap(g.fx, g.fy, g.cx, g.cy, kfs, points, lines, kidx, fg)
+    return SlamMap(g.fx, g.fy, g.cx, g.cy, kfs, points, lines, kidx, fg, lidx, n_kf - 1)
 
 
 # ------------------------------------------------------------------------------------ binding
@@ -187,7 +193,17 @@ HOST_EXPORTED = [
     "plslam_set_local", "plslam_set_full_graph", "plslam_get_full_graph", "plslam_kf_idx_set", "plslam_kf_idx_get",
     "plslam_local_ba_plucker_g2o", "plslam_get_keyframe", "plslam_get_point", "plslam_get_line",
     "plslam_pluker_to_orth", "plslam_orth_to_pluker",
+    "plslam_set_inlier", "plslam_set_params", "plslam_set_max_kf_idx", "plslam_kf_lines_idx_set", "plslam_kf_lines_idx_get",
+    "plslam_form_local_map", "plslam_remove_bad_landmarks_pluker", "plslam_local_mapping_step", "plslam_exists",
 ]
+
+
+@dataclasses.dataclass
+class SlamParams:
+    """SlamConfig values of the local-mapping step (src/slamConfig.cpp:48,61-62 defaults)."""
+    min_lm_obs: int = 5
+    min_lm_cov_graph: int = 75
+    min_kf_local_map: int = 3
 
 _hl = None
 
@@ -226,6 +242,15 @@ def load_host(path: Optional[str] = None):
     L.plslam_pluker_to_orth.restype = None
     L.plslam_orth_to_pluker.argtypes = [dp, dp]
     L.plslam_orth_to_pluker.restype = None
+    L.plslam_set_inlier.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32]
+    L.plslam_set_params.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32]
+    L.plslam_set_max_kf_idx.argtypes = [vp, C.c_int32]
+    L.plslam_kf_lines_idx_set.argtypes = [vp, C.c_int32, ip, C.c_int32]
+    L.plslam_kf_lines_idx_get.argtypes = [vp, C.c_int32, ip, C.c_int32, ip]
+    L.plslam_form_local_map.argtypes = [vp, C.c_int32]
+    L.plslam_remove_bad_landmarks_pluker.argtypes = [vp, ip, ip]
+    L.plslam_local_mapping_step.argtypes = [vp, C.c_int32, C.POINTER(PlslamLbaStats), ip, ip]
+    L.plslam_exists.argtypes = [vp, C.c_int32, C.c_int32, ip]
     for n in HOST_EXPORTED:
         if n not in ("plslam_map_last_error", "plslam_pluker_to_orth", "plslam_orth_to_pluker"):
             getattr(L, n).restype = C.c_int
@@ -241,7 +266,8 @@ def _d(a):
 class HostMap:
     """A MapHandler (C++ host mirror) holding a SlamMap."""
 
-    def __init__(self, m: SlamMap, corrected_line_jacobian: bool = False, device: int = 0):
+    def __init__(self, m: SlamMap, corrected_line_jacobian: bool = False, device: int = 0,
+                 params: Optional[SlamParams] = None):
         self.L = load_host()
         o = capi.PlbaOpts()
         from .lib import load
@@ -255,6 +281,8 @@ class HostMap:
         self.n_pt = len(m.points)
         self.n_ln = len(m.lines)
         self._push(m)
+        p = params or SlamParams()
+        self._check(self.L.plslam_set_params(self.h, p.min_lm_obs, p.min_lm_cov_graph, p.min_kf_local_map), "params")
 
     def _check(self, rc, what):
         if rc != 0:
@@ -312,11 +340,16 @@ class HostMap:
                                                                lm.kf_obs_list[i], op, s)
                     self._check(rc, "add landmark")
                 self._check(L.plslam_set_local(h, kind, lm.idx, int(lm.local)), "set_local")
+                self._check(L.plslam_set_inlier(h, kind, lm.idx, int(lm.inlier)), "set_inlier")
         fg = np.ascontiguousarray(m.full_graph, np.uint32)
         self._check(L.plslam_set_full_graph(h, fg.shape[0], fg.ctypes.data_as(C.POINTER(C.c_uint32))), "full_graph")
         for k, lst in m.map_points_kf_idx.items():
             a = np.asarray(lst, np.int32)
             self._check(L.plslam_kf_idx_set(h, k, a.ctypes.data_as(ip), len(a)), "kf_idx_set")
+        for k, lst in m.map_lines_kf_idx.items():
+            a = np.asarray(lst, np.int32)
+            self._check(L.plslam_kf_lines_idx_set(h, k, a.ctypes.data_as(ip), len(a)), "kf_lines_idx_set")
+        self._check(L.plslam_set_max_kf_idx(h, int(m.max_kf_idx)), "max_kf_idx")
 
     def set_solver(self, fn: Optional[Callable]):
         """fn(graph: PlbaGraph, result: PlbaResult) -> int, or None for the MI355X backend."""
@@ -341,6 +374,28 @@ class HostMap:
         self._check(self.L.plslam_local_ba_plucker_g2o(self.h, C.byref(st)), "local_ba_plucker_g2o")
         return st.as_dict()
 
+    def form_local_map(self, kf_idx: int):
+        self._check(self.L.plslam_form_local_map(self.h, kf_idx), "form_local_map")
+
+    def remove_bad_landmarks(self):
+        a, b = C.c_int32(), C.c_int32()
+        self._check(self.L.plslam_remove_bad_landmarks_pluker(self.h, C.byref(a), C.byref(b)), "remove_bad")
+        return a.value, b.value
+
+    def local_mapping_step(self, kf_idx: int) -> dict:
+        st = PlslamLbaStats()
+        a, b = C.c_int32(), C.c_int32()
+        self._check(self.L.plslam_local_mapping_step(self.h, kf_idx, C.byref(st), C.byref(a), C.byref(b)),
+                    "local_mapping_step")
+        d = st.as_dict()
+        d["points_removed"], d["lines_removed"] = a.value, b.value
+        return d
+
+    def exists(self, kind: int, idx: int) -> bool:
+        e = C.c_int32()
+        self._check(self.L.plslam_exists(self.h, kind, idx, C.byref(e)), "exists")
+        return bool(e.value)
+
     def read(self, like: SlamMap) -> SlamMap:
         """Read the map state back (same object layout as `like`)."""
         L, h = self.L, self.h
@@ -362,8 +417,11 @@ class HostMap:
             kf.ls_idx = [int(v) for v in li]
         dp, bp = C.POINTER(C.c_double), C.POINTER(C.c_uint8)
         for kind, lms in ((1, out.points), (2, out.lines)):
-            for lm in lms:
+            for j, lm in enumerate(lms):
                 if lm is None:
+                    continue
+                if not self.exists(kind, lm.idx):   # deleted by removeBadMapLandmarksForPluker
+                    lms[j] = None
                     continue
                 cap = len(lm.kf_obs_list) + len(lm.sigma_list) + 4
                 inl, loc, nobs = C.c_int32(), C.c_int32(), C.c_int32()
@@ -405,4 +463,9 @@ class HostMap:
             buf = np.zeros(4096, np.int32)
             self._check(L.plslam_kf_idx_get(h, k, buf.ctypes.data_as(ip), len(buf), C.byref(n)), "kf_idx_get")
             out.map_points_kf_idx[k] = [int(v) for v in buf[:n.value]]
+        for k in list(out.map_lines_kf_idx.keys()):
+            buf = np.zeros(4096, np.int32)
+            self._check(L.plslam_kf_lines_idx_get(h, k, buf.ctypes.data_as(ip), len(buf), C.byref(n)),
+                        "kf_lines_idx_get")
+            out.map_lines_kf_idx[k] = [int(v) for v in buf[:n.value]]
         return out

@@ -5,6 +5,8 @@ C++ host mirror, pl-slam-plucker_amd/host/):
   marshal    src/mapHandler.cpp:5931-6117   (A1b)
   outliers   src/mapHandler.cpp:6154-6293   (A1d)
   write-back src/mapHandler.cpp:6296-6319   (A1e)
+  formLocalMap(kf)                src/mapHandler.cpp:1073-1137   
+  removeBadMapLandmarksForPluker  src/mapHandler.cpp:3816-3897   (§8f row 3)
 
 operating on plba.slam_map.SlamMap objects. `solve` is any callable Graph -> result dict
 (a stub on CPU, the CPU oracle in GPU tests).
@@ -159,6 +161,64 @@ def lba(m: SlamMap, solve: Callable[[Graph], dict]) -> dict:
     return st
 
 
+def form_local_map(m: SlamMap, kf_idx: int, params) -> None:
+    """MapHandler::formLocalMap(KeyFrame*) (src/mapHandler.cpp:1073-1137)."""
+    for k in m.keyframes:
+        if k is not None:
+            k.local = False
+    for lm in m.points + m.lines:
+        if lm is not None:
+            lm.local = False
+
+    def mark(k):
+        for i in k.pt_idx:
+            if i != -1 and m.points[i] is not None:
+                m.points[i].local = True
+        for i in k.ls_idx:
+            if i != -1 and m.lines[i] is not None:
+                m.lines[i].local = True
+    kf = m.keyframes[kf_idx]
+    kf.local = True
+    mark(kf)
+    g_size = m.full_graph.shape[0] - 1
+    for i in range(g_size):
+        if int(m.full_graph[g_size, i]) >= params.min_lm_cov_graph or abs(g_size - i) <= params.min_kf_local_map:
+            m.keyframes[i].local = True
+            mark(m.keyframes[i])
+
+
+def remove_bad(m: SlamMap, params):
+    """MapHandler::removeBadMapLandmarksForPluker() (src/mapHandler.cpp:3816-3897)."""
+    removed = [0, 0]
+    for kind, lms, kidx in ((0, m.points, m.map_points_kf_idx), (1, m.lines, m.map_lines_kf_idx)):
+        for j, lm in enumerate(lms):
+            if lm is None:
+                continue
+            if not lm.local and m.max_kf_idx - lm.kf_obs_list[0] > 10 and \
+                    (not lm.inlier or len(lm.obs_list) < params.min_lm_obs):
+                kf_obs = lm.kf_obs_list[0]
+                feats = m.keyframes[kf_obs].pt_idx if kind == 0 else m.keyframes[kf_obs].ls_idx
+                for q, f in enumerate(feats):
+                    if f == lm.idx:
+                        feats[q] = -1
+                        break
+                lst = kidx[kf_obs]
+                if lm.idx in lst:
+                    lst.remove(lm.idx)          # first occurrence
+                lms[j] = None
+                removed[kind] += 1
+    return removed
+
+
+def local_mapping_step(m: SlamMap, kf_idx: int, solve, params) -> dict:
+    """localMappingThread's USE_LINE_PLUKER body after lookForCommonMatches
+    (src/mapHandler.cpp:1274-1279)."""
+    form_local_map(m, kf_idx, params)
+    st = lba(m, solve)
+    st["points_removed"], st["lines_removed"] = remove_bad(m, params)
+    return st
+
+
 def compare_maps(a: SlamMap, b: SlamMap, pose_tol=1e-9, lm_tol=1e-9):
     """Raises AssertionError on the first mismatch (bookkeeping exact, states to tolerance)."""
     for ka, kb in zip(a.keyframes, b.keyframes):
@@ -188,3 +248,4 @@ def compare_maps(a: SlamMap, b: SlamMap, pose_tol=1e-9, lm_tol=1e-9):
             assert d <= lm_tol * max(1.0, np.abs(y.pos).max()), (tag, "pos", d)
     assert np.array_equal(a.full_graph, b.full_graph), "full_graph"
     assert a.map_points_kf_idx == b.map_points_kf_idx, "map_points_kf_idx"
+    assert a.map_lines_kf_idx == b.map_lines_kf_idx, "map_lines_kf_idx"

@@ -211,3 +211,115 @@ def test_gpu_host_path_matches_model_with_oracle(cfg):
               "actually_bad_point_obs", "bad_line_obs", "actually_bad_line_obs", "iters"):
         assert st[k] == st_model[k], (k, st[k], st_model[k])
     hm.compare_maps(got, want, pose_tol=1e-4, lm_tol=1e-4)
+
+
+# ----------------------------------------------------------------- the local-mapping step
+# formLocalMap(kf) -> LBA -> removeBadMapLandmarksForPluker (src/mapHandler.cpp:1274-1279)
+from plba.slam_map import SlamParams  # noqa: E402
+
+
+def _step_params(m, kf_idx):
+    # a covisibility threshold inside the range of the last full_graph row, so both branches
+    # of the window test (:1117) are taken
+    row = m.full_graph[-1, :-1].astype(np.int64)
+    return SlamParams(min_lm_obs=4, min_lm_cov_graph=int(np.median(row)) + 1, min_kf_local_map=2)
+
+
+def _aged(m, extra=15):
+    m.max_kf_idx = len(m.keyframes) - 1 + extra   # every landmark's base KF is > 10 KFs old
+    return m
+
+
+@pytest.mark.parametrize("cfg,seed", [("C1L", 21), ("C1", 22)])
+def test_form_local_map_matches_model(cfg, seed):
+    m = make_map(synth.generate(cfg, fixed_frac=0.3), seed=seed)
+    for kf_idx in (len(m.keyframes) - 1, 3):
+        p = _step_params(m, kf_idx)
+        hmap = HostMap(m, params=p)
+        hmap.form_local_map(kf_idx)
+        want = m.copy()
+        hm.form_local_map(want, kf_idx, p)
+        got = hmap.read(m)
+        assert [k.local for k in got.keyframes] == [k.local for k in want.keyframes]
+        for a, b in zip(got.points + got.lines, want.points + want.lines):
+            assert (a is None) == (b is None)
+            if a is not None:
+                assert a.local == b.local, a.idx
+        assert any(k.local for k in want.keyframes) and not all(k.local for k in want.keyframes)
+
+
+@pytest.mark.parametrize("cfg,seed", [("C1L", 23), ("C1", 24)])
+def test_remove_bad_landmarks_matches_model(cfg, seed):
+    m = _aged(make_map(synth.generate(cfg, fixed_frac=0.3), seed=seed))
+    # some outliers and short tracks among the non-local landmarks
+    rng = np.random.default_rng(seed)
+    for lm in m.points + m.lines:
+        if lm is not None and rng.random() < 0.3:
+            lm.inlier = False
+        if lm is not None and rng.random() < 0.4:
+            lm.local = False
+    p = SlamParams(min_lm_obs=4)
+    hmap = HostMap(m, params=p)
+    npt, nln = hmap.remove_bad_landmarks()
+    want = m.copy()
+    rem = hm.remove_bad(want, p)
+    assert [npt, nln] == rem and npt > 0 and (nln > 0 or cfg == "C1")
+    hm.compare_maps(hmap.read(m), want, pose_tol=0, lm_tol=0)
+
+
+def test_local_mapping_step_matches_model():
+    m = _aged(make_map(synth.generate("C1L", fixed_frac=0.3), seed=25), extra=5)
+    kf_seq = [len(m.keyframes) - 1, len(m.keyframes) - 3]
+    p = _step_params(m, kf_seq[0])
+    hmap, _ = host_with(m, stub_solve)
+    hmap.L.plslam_set_params(hmap.h, p.min_lm_obs, p.min_lm_cov_graph, p.min_kf_local_map)
+    want = m.copy()
+    for kf_idx in kf_seq:
+        st = hmap.local_mapping_step(kf_idx)
+        st_model = hm.local_mapping_step(want, kf_idx, stub_solve, p)
+        for k, v in st_model.items():
+            assert st[k] == v, (k, st[k], v)
+    hm.compare_maps(hmap.read(m), want, pose_tol=1e-12, lm_tol=1e-12)
+
+
+def test_remove_bad_refuses_missing_kf_idx_key():
+    m = _aged(make_map(synth.generate("C1L", fixed_frac=0.3), seed=26))
+    for lm in m.lines:
+        lm.local, lm.inlier = False, False
+    del m.map_lines_kf_idx[m.lines[0].kf_obs_list[0]]   # .at() would throw in the reference
+    hmap = HostMap(m)
+    with pytest.raises(Exception, match="PLBA_E_STATE"):
+        hmap.remove_bad_landmarks()
+    got = hmap.read(m)
+    assert all(a is not None for a in got.points + got.lines if a is not None) and \
+        sum(a is None for a in got.lines) == 0
+
+
+def test_form_local_map_refuses_missing_covisible_keyframe():
+    m2 = make_map(synth.generate("C1L", fixed_frac=0.3), seed=27)
+    m2.keyframes[2] = None   # a NULL slot the reference would dereference (:1120)
+    for lm in m2.points + m2.lines:
+        if lm is not None and 2 in lm.kf_obs_list:
+            lm.local = False
+    hmap2 = HostMap(m2, params=SlamParams(min_kf_local_map=100))   # every KF is in the window
+    before = hmap2.read(m2)
+    with pytest.raises(Exception, match="PLBA_E_INVALID"):
+        hmap2.form_local_map(len(m2.keyframes) - 1)
+    after = hmap2.read(m2)
+    assert [k.local if k else None for k in after.keyframes] == [k.local if k else None for k in before.keyframes]
+
+
+@pytest.mark.gpu
+def test_gpu_local_mapping_step_matches_model_with_oracle():
+    import oracle_api as oa
+    m = _aged(make_map(synth.generate("C2", fixed_frac=0.2), seed=28), extra=5)
+    kf = len(m.keyframes) - 1
+    p = _step_params(m, kf)
+    hmap = HostMap(m, params=p)
+    st = hmap.local_mapping_step(kf)
+    want = m.copy()
+    st_model = hm.local_mapping_step(want, kf, lambda gg: oa.lba_plucker(gg), p)
+    for k in ("n_free_kf", "n_fixed_kf", "n_ept", "n_eln", "bad_point_obs", "actually_bad_point_obs",
+              "bad_line_obs", "actually_bad_line_obs", "iters", "points_removed", "lines_removed"):
+        assert st[k] == st_model[k], (k, st[k], st_model[k])
+    hm.compare_maps(hmap.read(m), want, pose_tol=1e-4, lm_tol=1e-4)
