@@ -618,8 +618,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_any, d.n_lm_blocks);
     ALLOC(d.part_max, nf + d.n_lm_blocks);
     ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * 27);
-    ALLOC(d.part_lm, std::max(d.n_lin_blocks, d.n_lm_blocks));
-    ALLOC(d.Xplk, (size_t)n_lm * 6);
+    ALLOC(d.part_lm, std::max(d.n_lms_blocks, 1));
     ALLOC(d.part_lms, d.n_lms_blocks);
     ALLOC(d.part_ps, d.n_kf_blocks);
     ALLOC(d.ctrl, 1);
@@ -711,7 +710,6 @@ int allreduce(plba_ctx *ctx, const double *send, double *recv, size_t n) {
 int launch_step(plba_ctx *ctx) {
     Dev &d = ctx->d;
     hipStream_t s = ctx->stream;
-    const int nv = std::max(std::max(d.n_lm, d.n_kf), 1);
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     if (d.nf > 0 || d.n_lm > 0) {
         const int nred = kPoseParts * d.nf + (d.n_lm > 0 ? d.n_lm_blocks : 0);
@@ -740,7 +738,6 @@ int launch_step(plba_ctx *ctx) {
     if (d.n == 0 && d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(1), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) {
         LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lms_blocks), dim3(kLmsNT), 0, s, d));
-        LAUNCH(K_EVAL, hipLaunchKernelGGL(k_edge_eval, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }
     if (d.sharded) {
         LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide_pack, dim3(1), dim3(kBlock), 0, s, d));

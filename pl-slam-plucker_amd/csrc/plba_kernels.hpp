@@ -20,8 +20,8 @@
 //                      k_rcs_factor_band<BW> (one sweep) and the dense k_rcs_factor (bw>20)
 //                      are the fallbacks
 //                      ... each ending with the pose oplus of the free poses (pose_update_wg)
-//   k_lm_solve         landmark-parallel: x_l = L⁻ᵀL⁻¹(b_l − Σ_e B_eᵀA_e x_p), oplus, Σx(λx+b) partials
-//   k_edge_eval        edge-parallel: χ² at the trial state, robust partial sums
+//   k_lm_solve         landmark-parallel: x_l = L⁻ᵀL⁻¹(b_l − Σ_e B_eᵀA_e x_p), oplus, Σx(λx+b)
+//                      partials, then the landmark's edges' χ² at the trial state (robust partials)
 //   k_decide           ρ, accept/reject, λ/ν update, optimize() loop control (g2o Levenberg)
 //                      (accepting flips Ctrl::cur: the trial buffer becomes the current state)
 // After the schedule: k_refresh (level-1 computeError) and k_depth (isDepthPositive).
@@ -113,8 +113,7 @@ struct Dev {
     double *part_chi2;                  // [n_lin_blocks]
     int32_t *part_any;                  // [n_lm_blocks] block has an active landmark
     double *part_max;                   // [nf + n_lm_blocks] (landmark part from nf on)
-    double *part_lm, *part_lms;         // [n_lin_blocks] trial χ² partials, [n_lm_blocks] scale partials
-    double *Xplk;                       // [n_lm][6] trial Plücker of lines (xyz of points)
+    double *part_lm, *part_lms;         // [n_lms_blocks] trial χ² partials, scale partials (k_lm_solve)
     double *part_ps;                    // [n_kf_blocks]
     Ctrl *ctrl;
     plba_iter_trace *trace;             // [kTraceCap] per-iteration records written by k_decide
@@ -975,8 +974,9 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
     int sk = 0, kR = 0, kRK = 1;                  // k % W, k % R, (k+1) % RK
+    // a zero pivot sets s_fail and the sweep runs on (inf/NaN blocks are never used: the
+    // caller drops the solve); no per-step LDS read of the flag on the critical chain
     for (int k = 0; k < nsteps; ++k) {
-        if (s_fail) break;
         const int kb = k & 1;
         const int wmax = min(BW, nrows - 1 - k);
         const double *Kk = Kv + kb * 36;
@@ -1544,6 +1544,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
     const bool live = l < d.n_lm;
     const bool act = live && d.lm_active[l] != 0;
     const bool solve = d.ctrl->solve_ok != 0;
+    double chi = 0.0;  // this lane's robust χ² at the trial state
     // r = b_l − Σ_e Hpl_eᵀ x_p,  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)  (edges of a fixed pose: 0)
     double u[4] = {0, 0, 0, 0};
     if (act && solve) {
@@ -1603,63 +1604,55 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
                 for (int i = 0; i < 4; ++i) x[i] = d.xl[(size_t)l * 4 + i];
             }
             if (q < DIM) sc = x[q] * (lam * x[q] + d.bl[(size_t)l * 4 + q]);
-            double X[4];
+            double X[4], Lp[6];
             if (pt) {
                 X[0] = Xc[0] + x[0]; X[1] = Xc[1] + x[1]; X[2] = Xc[2] + x[2]; X[3] = 0.0;
             } else {
                 const double in[4] = {Xc[0], Xc[1], Xc[2], Xc[3]};
                 orth_oplus(in, x, X);
-                double Lp[6];
                 orth_to_pluker(X, Lp);
-                if (q < 3) {
-                    d.Xplk[(size_t)l * 6 + 2 * q] = Lp[2 * q];
-                    d.Xplk[(size_t)l * 6 + 2 * q + 1] = Lp[2 * q + 1];
-                }
             }
             Xt[q] = X[q];
+            // the landmark's edges at the trial state (computeActiveErrors of the trial), from
+            // the estimate in registers; lane q takes edges q, q+4, ... (the trial poses were
+            // written by the factorisation kernel)
+            const bool robust = d.ctrl->robust != 0;
+            const double delta = pt ? d.huber_pt : d.huber_ln;
+            for (int e = d.lm_off[l] + q; e < d.lm_off[l + 1]; e += kLmLanes) {
+                if (!d.e_active[e]) continue;
+                const double *T = Ttrial(d) + (size_t)d.e_kf[e] * 12;
+                const double *obs = d.e_obs + (size_t)e * 4;
+                double err[2];
+                if (pt) {
+                    double z;
+                    point_error(T, X, obs, d.cam, err, z);
+                } else {
+                    line_error(T, Lp, obs, d.cam, err);
+                }
+                const double info = d.e_info[e];
+                const double c2 = err[0] * (info * err[0]) + err[1] * (info * err[1]);
+                d.chi2_last[e] = c2;
+                double rho0 = c2, rho1;
+                if (robust) huber(c2, delta, rho0, rho1);
+                chi += rho0;
+            }
         } else {
             Xt[q] = Xc[q];
         }
     }
     const double s2 = block_sum<kLmsNT>(sc, sh);
-    if (threadIdx.x == 0) d.part_lms[blockIdx.x] = s2;
-}
-// per edge: χ² at the trial state (last-evaluated semantics), robust partial sums
-__global__ __launch_bounds__(kBlock) void k_edge_eval(Dev d) {
-    TRIAL_GUARD
-    __shared__ double sh[kBlock / 64];
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    double chi = 0.0;
-    if (e < d.E && d.e_active[e]) {
-        const int l = d.e_lm[e];
-        const double *T = Ttrial(d) + (size_t)d.e_kf[e] * 12;
-        const double *obs = d.e_obs + (size_t)e * 4;
-        double err[2], delta;
-        if (e < d.Ep) {
-            double z;
-            point_error(T, Xtrial(d) + (size_t)l * 4, obs, d.cam, err, z);
-            delta = d.huber_pt;
-        } else {
-            line_error(T, d.Xplk + (size_t)l * 6, obs, d.cam, err);
-            delta = d.huber_ln;
-        }
-        const double info = d.e_info[e];
-        const double c2 = err[0] * (info * err[0]) + err[1] * (info * err[1]);
-        d.chi2_last[e] = c2;
-        double rho0 = c2, rho1;
-        if (d.ctrl->robust) huber(c2, delta, rho0, rho1);
-        chi = rho0;
+    const double s1 = block_sum<kLmsNT>(chi, sh);
+    if (threadIdx.x == 0) {
+        d.part_lms[blockIdx.x] = s2;
+        d.part_lm[blockIdx.x] = s1;
     }
-    const double s1 = block_sum<kBlock>(chi, sh);
-    if (threadIdx.x == 0) d.part_lm[blockIdx.x] = s1;
 }
-
 // sharded: this rank's trial χ² and landmark scale terms into the all-reduced decision array
 __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
     TRIAL_GUARD
     __shared__ double sh[kBlock / 64];
     double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
+    for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) a += d.part_lm[i];
     for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) b += d.part_lms[i];
     const double ta = block_sum<kBlock>(a, sh);
     const double tb = block_sum<kBlock>(b, sh);
@@ -1675,7 +1668,7 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
     __shared__ double sh[kBlock / 64];
     double a = 0.0, b = 0.0;
     if (!d.sharded) {
-        for (int i = threadIdx.x; i < d.n_lin_blocks; i += kBlock) a += d.part_lm[i];
+        for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) a += d.part_lm[i];
         for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) b += d.part_lms[i];
     }
     for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];  // poses: replicated

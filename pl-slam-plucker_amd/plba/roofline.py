@@ -60,9 +60,8 @@ def kernel_bytes(g: Graph, name: str, st: dict) -> float:
         return g.n_kf * (12 + 12) * F + nf * 12 * F
     if name == "k_lm_solve":
         # per landmark: X (4), b_l (4), Hll (10) in, X_trial (4), x_l (4) out; per free edge the
-        # back-substitution reads A (12) and B (8); x_p once
-        return n_lm * (4 + 4 + 10 + 4 + 4) * F + n_lm * I + Ef * (I + (12 + 8) * F) + nf * 6 * F
-    if name == "k_edge_eval":
-        rd = Ep * (2 * I + 2 * F + F + 1) + El * (2 * I + 4 * F + F + 1)
-        return rd + g.n_kf * 12 * F + g.n_pt * 3 * F + g.n_ln * 4 * F + E * F
+        # back-substitution reads A (12) and B (8); x_p once; then the trial evaluation of every
+        # edge: pose index, active flag, obs (2|4), info in, χ² out; trial poses once
+        ev = Ep * (I + 1 + 2 * F + F) + El * (I + 1 + 4 * F + F) + E * F + g.n_kf * 12 * F
+        return n_lm * (4 + 4 + 10 + 4 + 4) * F + n_lm * I + Ef * (I + (12 + 8) * F) + nf * 6 * F + ev
     return 0.0
