@@ -181,6 +181,10 @@ void shard_plan(const plba_graph *g, int R, int32_t *pt_owner, int32_t *ln_owner
     }
 }
 
+inline bool env_flag(const char *name) {
+    const char *v = getenv(name);
+    return v && v[0] == '1';
+}
 inline size_t band_lds_bytes(int bw) { return sizeof(double) * band_lds_doubles(bw, 0); }
 template <int... B>
 const void *band_kernel_impl(int bw, std::integer_sequence<int, B...>) {
@@ -210,8 +214,25 @@ inline size_t band_lds_bytes(int bw, int nf) { return sizeof(double) * band_lds_
 inline size_t twisted_lds_bytes(int bw, int nf) {
     return band_lds_bytes(bw, nf) + sizeof(double) * (twisted_extra_doubles(bw) + (size_t)nf * 6);  // + x_p staging
 }
+template <int... B>
+const void *cl_kernel_impl(int bw, bool twisted, std::integer_sequence<int, B...>) {
+    const void *k = nullptr;
+    ((bw == B ? (k = twisted ? (const void *)k_rcs_factor_twisted_cl<B> : (const void *)k_rcs_factor_band_cl<B>, 0) : 0),
+     ...);
+    return k;
+}
+// column-lane factorisation (plba_band_cl.hpp) for bandwidths up to kClMaxBW
+inline bool use_cl(int bw) { return bw >= 1 && bw <= kClMaxBW && !env_flag("PLBA_NO_CL"); }
+inline size_t cl_lds_bytes(int bw, int nf, bool twisted) {
+    return sizeof(double) * (cl_lds_doubles(bw) + (twisted ? (size_t)nf * 6 : 0));
+}
 inline void launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
+    if (d.cl) {
+        const void *k = cl_kernel_impl(d.bw, d.twisted != 0, std::make_integer_sequence<int, kClMaxBW + 1>{});
+        (void)hipLaunchKernel(k, dim3(d.twisted ? 2 : 1), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
+        return;
+    }
     if (d.twisted)
         (void)hipLaunchKernel(twisted_kernel(d.bw), dim3(2), dim3(kBandNT), args, twisted_lds_bytes(d.bw, d.nf), s);
     else
@@ -517,8 +538,11 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // two-sided factorisation when the chain is long enough to halve and the separator's dense
     // system fits next to the band window in LDS (PLBA_NO_TWIST=1 disables, diagnostics only)
     const char *no_twist = getenv("PLBA_NO_TWIST");
+    const bool cl = band_mode && use_cl(bw);
     const bool twisted = band_mode && bw >= 1 && nf >= 2 * bw + 16 &&
-                         twisted_lds_bytes(bw, nf) <= 159 * 1024 && !(no_twist && no_twist[0] == '1');
+                         (cl ? cl_lds_bytes(bw, nf, true) : twisted_lds_bytes(bw, nf)) <= 159 * 1024 &&
+                         !(no_twist && no_twist[0] == '1');
+    d.cl = cl && cl_lds_bytes(bw, nf, twisted) <= 159 * 1024 ? 1 : 0;
     d.twisted = twisted ? 1 : 0;
     d.tw_m = twisted ? (nf - bw) / 2 : 0;
     d.corrected = ctx->opts.corrected_line_jacobian;
@@ -1186,10 +1210,10 @@ int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [17][8] */) {
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[13] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+    const int64_t v[14] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
-                           ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted};
-    for (int i = 0; i < cap && i < 13; ++i) out[i] = v[i];
+                           ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl};
+    for (int i = 0; i < cap && i < 14; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

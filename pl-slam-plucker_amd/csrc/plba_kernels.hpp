@@ -130,6 +130,7 @@ struct Dev {
     int32_t *lm_gpos, *e_gpos;          // local landmark / edge -> whole-window position
     double *gat;                        // [n_lm_g*4 + 3*E_g] final gather buffer
     // two-sided banded factorisation (k_rcs_factor_twisted)
+    int32_t cl;                         // column-lane factorisation (plba_band_cl.hpp)
     int32_t twisted, tw_m;              // enabled; rows 0..tw_m-1 top-down, separator tw_m..tw_m+bw-1
     double *Bd2, *bs2;                  // block-reversed band / rhs (row r' = nf-1-i)
     double *Lband2, *Kinv2, *zb2;       // factors of the bottom segment (reversed numbering)
@@ -1133,7 +1134,10 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
 template <int BW, bool LX = false>
 __device__ __forceinline__ void band_backward_rl(const double *Lband, const double *zb, int nsteps, int nrows,
                                                  const double *xsep, double *xp, bool reversed, int nf, int lane) {
-    constexpr int W = BW + 1, kPipe = 4;
+#ifndef PLBA_BWD_PIPE
+#define PLBA_BWD_PIPE 4
+#endif
+    constexpr int W = BW + 1, kPipe = PLBA_BWD_PIPE;
     if (nsteps <= 0) return;
     const int G = lane / 6, r = lane % 6;      // lane group G holds the window row j ≡ G (mod BW)
     const bool act = lane < BW * 6;
@@ -1435,6 +1439,8 @@ template <int BW>
 __global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d) {
     if constexpr (BW >= 1) k_rcs_factor_twisted_body<BW>(d);  // (the host never selects bw 0)
 }
+
+#include "plba_band_cl.hpp"
 
 // ---------------------------------------------------------------- update + trial evaluation
 // stand-alone pose update (windows without free poses: no factorisation kernel to fuse into)

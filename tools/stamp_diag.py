@@ -24,14 +24,24 @@ nf = int((g.kf_fixed == 0).sum())
 st = s.structure_stats()
 steps_per_trial = (nf - st["bw"]) // 2 if st["twisted"] else nf
 print(cfg, "rc", rc, "trials", ntr, "forward steps per trial", steps_per_trial, "twisted", st["twisted"])
+if st.get("column_lane"):
+    names = ["A:publish", "B:gauss-jordan", "C:publish-X", "barrier", "EF:next-column", "prefetch",
+             "w:rhs", "w:flush"]
+    wnames = ["-", "-", "-", "barrier", "w:rowload", "w:pairs", "w:rhs", "w:flush"]
 for w in range(16):
     if a[w].sum() == 0:
         continue
     per = a[w] / (ntr * steps_per_trial)
-    print(f"wave {w:2d} cycles/step: " + " ".join(f"{n}={v:.0f}" for n, v in zip(names, per)), f"total={per.sum():.0f}")
+    nm = wnames if st.get("column_lane") and w > 0 else names
+    print(f"wave {w:2d} cycles/step: " + " ".join(f"{n}={v:.0f}" for n, v in zip(nm, per) if n != "-"),
+          f"total={per.sum():.0f}")
 
 tw = a[16]
-if tw[4] > 0:
+if st.get("column_lane") and st["twisted"]:
+    n = ntr
+    print(f"column-lane twisted (per launch): fwd seg0 {tw[0]/n:.0f} fwd seg1 {tw[1]/n:.0f} wait+merge {tw[2]/n:.0f} "
+          f"separator steps {tw[3]/n:.0f} backward {tw[4]/n:.0f}")
+elif tw[4] > 0:
     n = tw[4]
     print(f"twisted (per launch, s_memtime/readcyclecounter units): fwd seg0 {tw[0]/n:.0f} fwd seg1 {tw[1]/n:.0f} "
           f"handoff+separator {tw[2]/n:.0f} backward {tw[3]/n:.0f}")
