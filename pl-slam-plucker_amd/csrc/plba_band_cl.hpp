@@ -144,8 +144,13 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
                 wave_lds_sync();
 #endif
                 double a1[36];
+#ifdef PLBA_CL_NOA1  // timing experiment only: wrong results
+#pragma unroll
+                for (int q = 0; q < 36; ++q) a1[q] = 1e-3 * q;
+#else
 #pragma unroll
                 for (int q = 0; q < 36; ++q) a1[q] = pA[s1 * 36 + q];
+#endif
                 STAMP(0);
                 // B: Gauss–Jordan on block row k across the lanes (pivot lanes 6*sk + p)
 #pragma unroll
@@ -307,7 +312,7 @@ __device__ __forceinline__ void cl_store_sep(const double *lds, int k1, double *
 template <int BW>
 __global__ __launch_bounds__(kClNT) void k_rcs_factor_band_cl(Dev d) {
     TRIAL_GUARD
-    extern __shared__ double lds[];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_fail;
     if constexpr (BW >= 1 && BW <= kClMaxBW) {
         const BandSeg g{d.Bd, d.bs, d.Lband, nullptr, d.zb, d.nf, d.nf, nullptr};
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_band_cl(Dev d) {
 template <int BW>
 __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d) {
     TRIAL_GUARD
-    extern __shared__ double lds[];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_fail;
     if constexpr (BW >= 1 && BW <= kClMaxBW) {
         constexpr int W = BW + 1;

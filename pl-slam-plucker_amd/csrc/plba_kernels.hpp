@@ -1264,7 +1264,7 @@ __device__ __forceinline__ void band_backward(const double *Lband, const double 
 template <int BW>
 __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
     TRIAL_GUARD
-    extern __shared__ double lds[];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     const BandSeg g{d.Bd, d.bs, d.Lband, d.Kinv, d.zb, d.nf, d.nf, nullptr};
     const bool fail = band_forward<BW>(g, lds, d.ring, d.stamps);
     if (threadIdx.x == 0) d.ctrl->solve_ok = fail ? 0 : 1;
@@ -1289,7 +1289,7 @@ template <int BW>
 __device__ __forceinline__ void k_rcs_factor_twisted_body(Dev &d) {
     TRIAL_GUARD
     constexpr int W = BW + 1, NT = kBandNT, NS = 6 * BW, LD = NS + 1;
-    extern __shared__ double lds[];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_last, s_sfail;
     const int seg = blockIdx.x, tid = threadIdx.x;
     const size_t sep_stride = (size_t)BW * W * 36 + (size_t)BW * 6;
@@ -1537,6 +1537,61 @@ __device__ __forceinline__ double quad_sum(double v) {
     return v + dpp_f64<0x4E>(v);
 }
 
+// v[q] for a lane-dependent q without dynamic register indexing (which spills the array to
+// scratch)
+__device__ __forceinline__ double sel4(const double (&v)[4], int q) {
+    // a select chain is turned back into an indexed scratch load by the compiler: blend instead
+    const double m0 = q == 0 ? 1.0 : 0.0, m1 = q == 1 ? 1.0 : 0.0, m2 = q == 2 ? 1.0 : 0.0, m3 = q == 3 ? 1.0 : 0.0;
+    return fma(v[3], m3, fma(v[2], m2, fma(v[1], m1, v[0] * m0)));
+}
+
+// value of quad lane Q in every lane of the quad (DPP quad_perm [Q,Q,Q,Q])
+template <int Q>
+__device__ __forceinline__ double quad_bcast(double v) {
+    return dpp_f64<Q | (Q << 2) | (Q << 4) | (Q << 6)>(v);
+}
+
+// VertexLMLineOrth::oplusImpl (g2o_types/g2o_types.h:72-130) followed by changeOrthToPluker
+// (g2o_types.h:367-387) for one line, with the transcendentals spread over the landmark's quad:
+// lane q evaluates sincos of θ_q and δθ_q (θ_3 = φ), the quad exchanges them by DPP, every lane
+// forms U' = R_xyz(θ)·Rx(δθ1)·Ry(δθ2)·Rz(δθ3) and W10 redundantly, lane q takes angle q of the
+// result with the reference's own function (atan2 / asin / atan2 / asin) and its sincos, and the
+// quad exchanges those to rebuild the Plücker vector from the new angles exactly as the
+// reference does: 3 sincos + 1 inverse per lane instead of 28 calls, same formulas.
+// Returns angle q of the new state. All four lanes of the quad must be active.
+__device__ __forceinline__ double orth_oplus_quad(const double (&D)[4], const double (&dD)[4], int q, double (&Lp)[6]) {
+    const double a = sel4(D, q), b = sel4(dD, q);
+    double sa, ca, sb, cb;
+    sincos(a, &sa, &ca);
+    sincos(b, &sb, &cb);
+    const double s1 = quad_bcast<0>(sa), c1 = quad_bcast<0>(ca), s2 = quad_bcast<1>(sa), c2 = quad_bcast<1>(ca);
+    const double s3 = quad_bcast<2>(sa), c3 = quad_bcast<2>(ca), w2 = quad_bcast<3>(sa), w1 = quad_bcast<3>(ca);
+    const double sx = quad_bcast<0>(sb), cx = quad_bcast<0>(cb), sy = quad_bcast<1>(sb), cy = quad_bcast<1>(cb);
+    const double sz = quad_bcast<2>(sb), cz = quad_bcast<2>(cb), sp = quad_bcast<3>(sb), cp = quad_bcast<3>(cb);
+    const double R[9] = {c2 * c3, s1 * s2 * c3 - c1 * s3, c1 * s2 * c3 + s1 * s3,
+                         c2 * s3, s1 * s2 * s3 + c1 * c3, c1 * s2 * s3 - s1 * c3,
+                         -s2,     s1 * c2,                c1 * c2};
+    const double Rx[9] = {1, 0, 0, 0, cx, -sx, 0, sx, cx};
+    const double Ry[9] = {cy, 0, sy, 0, 1, 0, -sy, 0, cy};
+    const double Rz[9] = {cz, -sz, 0, sz, cz, 0, 0, 0, 1};
+    double T1[9], T2[9], Rn[9];
+    mat3mul(R, Rx, T1);
+    mat3mul(T1, Ry, T2);
+    mat3mul(T2, Rz, Rn);
+    const double W10 = w2 * cp + w1 * sp;
+    double o;
+    if (q & 1) o = asin(q == 1 ? -Rn[6] : W10);
+    else o = q == 0 ? atan2(Rn[7], Rn[8]) : atan2(Rn[3], Rn[0]);
+    double so, co;
+    sincos(o, &so, &co);
+    const double t1 = quad_bcast<0>(so), u1 = quad_bcast<0>(co), t2 = quad_bcast<1>(so), u2 = quad_bcast<1>(co);
+    const double t3 = quad_bcast<2>(so), u3 = quad_bcast<2>(co), v2 = quad_bcast<3>(so), v1 = quad_bcast<3>(co);
+    // rot_xyz(new angles), columns 0 and 1 (plba_math.hpp), scaled by cos φ' / sin φ'
+    Lp[0] = v1 * (u2 * u3); Lp[1] = v1 * (u2 * t3); Lp[2] = v1 * (-t2);
+    Lp[3] = v2 * (t1 * t2 * u3 - u1 * t3); Lp[4] = v2 * (t1 * t2 * t3 + u1 * u3); Lp[5] = v2 * (t1 * u2);
+    return o;
+}
+
 // kLmLanes lanes per landmark: lane q walks edges q, q+4, ... of the landmark's CSR range for
 // the back-substitution sum, the quad adds the partials (DPP, fixed order), and every lane of
 // the quad then solves the 3x3/4x4 system redundantly; lane q writes component q.
@@ -1604,21 +1659,45 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
                             if (p < DIM) t -= L[pk(p, i)] * x[p];
                         x[i] = t / L[pk(i, i)];
                     }
-                d.xl[(size_t)l * 4 + q] = x[q];
+                if (q == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) d.xl[(size_t)l * 4 + i] = x[i];
+                }
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) x[i] = d.xl[(size_t)l * 4 + i];
             }
-            if (q < DIM) sc = x[q] * (lam * x[q] + d.bl[(size_t)l * 4 + q]);
+            if (q == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (i < DIM) sc += x[i] * (lam * x[i] + d.bl[(size_t)l * 4 + i]);
+            }
             double X[4], Lp[6];
             if (pt) {
                 X[0] = Xc[0] + x[0]; X[1] = Xc[1] + x[1]; X[2] = Xc[2] + x[2]; X[3] = 0.0;
+                if (q == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) Xt[i] = X[i];
+                }
             } else {
                 const double in[4] = {Xc[0], Xc[1], Xc[2], Xc[3]};
+#if defined(PLBA_DBG_V1)
+                double Lq[6];
+                const double oq = orth_oplus_quad(in, x, q, Lq);
                 orth_oplus(in, x, X);
                 orth_to_pluker(X, Lp);
+                Xt[q] = X[q];
+                if (fabs(oq - X[q]) > 1e-9)
+                    printf("DBG l=%d q=%d in=%.17g %.17g %.17g %.17g x=%.17g %.17g %.17g %.17g oq=%.17g X=%.17g\n", l, q,
+                           in[0], in[1], in[2], in[3], x[0], x[1], x[2], x[3], oq, X[q]);
+#elif defined(PLBA_DBG_V2)
+                orth_oplus(in, x, X);
+                Xt[q] = X[q];
+                (void)orth_oplus_quad(in, x, q, Lp);
+#else
+                Xt[q] = orth_oplus_quad(in, x, q, Lp);
+#endif
             }
-            Xt[q] = X[q];
             // the landmark's edges at the trial state (computeActiveErrors of the trial), from
             // the estimate in registers; lane q takes edges q, q+4, ... (the trial poses were
             // written by the factorisation kernel)
