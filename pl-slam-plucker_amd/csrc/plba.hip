@@ -546,6 +546,10 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.twisted = twisted ? 1 : 0;
     d.tw_m = twisted ? (nf - bw) / 2 : 0;
     d.corrected = ctx->opts.corrected_line_jacobian;
+    {  // timing experiments only (wrong results): PLBA_DIAG bit mask read by some kernels
+        const char *dg = getenv("PLBA_DIAG");
+        d.diag = dg ? atoi(dg) : 0;
+    }
     d.cam = Cam{g->fx, g->fy, g->cx, g->cy};
     d.huber_pt = g->huber_pt;
     d.huber_ln = g->huber_ln;

@@ -38,7 +38,10 @@ namespace plba {
 
 constexpr int kBlock = 256;
 constexpr int kLmBlock = 64;  // landmark-parallel kernels: 24k landmarks at C3 -> 375 workgroups, not 94
-constexpr int kChunk = 128;  // Schur triples per assembly wave (2 per lane)
+#ifndef PLBA_CHUNK
+#define PLBA_CHUNK 256
+#endif
+constexpr int kChunk = PLBA_CHUNK;  // Schur triples per assembly wave (4 per lane)
 constexpr int kTraceCap = 64;
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
 constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window factorisation holds
@@ -131,6 +134,7 @@ struct Dev {
     double *gat;                        // [n_lm_g*4 + 3*E_g] final gather buffer
     // two-sided banded factorisation (k_rcs_factor_twisted)
     int32_t cl;                         // column-lane factorisation (plba_band_cl.hpp)
+    int32_t diag;                       // PLBA_DIAG timing-experiment bits (0 in every real run)
     int32_t twisted, tw_m;              // enabled; rows 0..tw_m-1 top-down, separator tw_m..tw_m+bw-1
     double *Bd2, *bs2;                  // block-reversed band / rhs (row r' = nf-1-i)
     double *Lband2, *Kinv2, *zb2;       // factors of the bottom segment (reversed numbering)
@@ -1597,55 +1601,150 @@ __device__ __forceinline__ double orth_oplus_quad(const double (&D)[4], const do
 // the quad then solves the 3x3/4x4 system redundantly; lane q writes component q.
 constexpr int kLmLanes = 4;
 constexpr int kLmsNT = 256;  // k_lm_solve workgroup: 64 landmarks
+// Edge slots held in registers per lane (lane q: edges q, q+4, ... up to kLmSlots of them);
+// longer tracks fall back to a loop for the remainder. Every load of the kernel that does not
+// depend on another load is issued up front, so a landmark costs two dependent global round
+// trips (CSR offsets -> edge records, then x_p / trial poses) instead of one per phase.
+constexpr int kLmSlots = 2;
+struct LmEdge {
+    int e, h, kf;
+    bool act;
+    double info, obs[4], A[12], B[8];
+};
+__device__ __forceinline__ void lm_load_edge(const Dev &d, int e, LmEdge &s) {
+    s.e = e;
+    s.h = d.e_hidx[e];
+    s.kf = d.e_kf[e];
+    s.act = d.e_active[e] != 0;
+    s.info = d.e_info[e];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s.obs[k] = d.e_obs[(size_t)e * 4 + k];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) s.A[k] = d.A[(size_t)e * 12 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s.B[k] = d.B[(size_t)e * 8 + k];
+}
+// u += B_eᵀ (A_e x_p) for an edge of a free pose
+__device__ __forceinline__ void lm_hpl_x(const LmEdge &s, const double (&x)[6], double (&u)[4]) {
+    double ax0 = 0, ax1 = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        ax0 += s.A[k] * x[k];
+        ax1 += s.A[6 + k] * x[k];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] += s.B[i] * ax0 + s.B[4 + i] * ax1;
+}
+// robust χ² of one active edge at the trial state (computeActiveErrors)
+__device__ __forceinline__ double lm_eval(const Dev &d, const LmEdge &s, const double *T, bool pt, const double (&X)[4],
+                                          const double (&Lp)[6], bool robust, double delta) {
+    double err[2];
+    if (pt) {
+        double z;
+        point_error(T, X, s.obs, d.cam, err, z);
+    } else {
+        line_error(T, Lp, s.obs, d.cam, err);
+    }
+    const double c2 = err[0] * (s.info * err[0]) + err[1] * (s.info * err[1]);
+    d.chi2_last[s.e] = c2;
+    double rho0 = c2, rho1;
+    if (robust) huber(c2, delta, rho0, rho1);
+    return rho0;
+}
+
 __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
     TRIAL_GUARD
     __shared__ double sh[kLmsNT / 64];
     const int gt = blockIdx.x * kLmsNT + threadIdx.x;
     const int l = gt / kLmLanes, q = gt % kLmLanes;   // a quad never straddles a wave
     const bool live = l < d.n_lm;
-    const bool act = live && d.lm_active[l] != 0;
-    const bool solve = d.ctrl->solve_ok != 0;
-    double chi = 0.0;  // this lane's robust χ² at the trial state
+    const int lc = live ? l : 0;
+    const Ctrl *cg = d.ctrl;
+    const bool solve = cg->solve_ok != 0;
+    const bool robust = cg->robust != 0;
+    const double lam = cg->lambda;
+    const int cur = cg->cur;
+    // ---- round 1: landmark record + this lane's edge slots
+    const bool act = live && d.lm_active[lc] != 0;
+    const int off0 = d.lm_off[lc], off1 = d.lm_off[lc + 1];
+    double Xc[4], bl[4], H[10];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Xc[k] = d.Xb[cur][(size_t)lc * 4 + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bl[k] = d.bl[(size_t)lc * 4 + k];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) H[k] = d.Hll[(size_t)lc * 10 + k];
+    LmEdge sl[kLmSlots];
+    bool sv[kLmSlots];
+#pragma unroll
+    for (int j = 0; j < kLmSlots; ++j) {
+        const int e = off0 + q + kLmLanes * j;
+        sv[j] = act && e < off1;
+        lm_load_edge(d, sv[j] ? e : 0, sl[j]);
+    }
+    // ---- round 2: x_p of each slot's free pose, the slot's trial pose
+    const double *Tt0 = d.Tb[cur ^ 1];
+    double xs[kLmSlots][6], Ts[kLmSlots][12];
+#pragma unroll
+    for (int j = 0; j < kLmSlots; ++j) {
+        const int h = max(sl[j].h, 0);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) xs[j][k] = d.xp[6 * h + k];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Ts[j][k] = Tt0[(size_t)sl[j].kf * 12 + k];
+    }
+    double chi = 0.0, sc = 0.0;
     // r = b_l − Σ_e Hpl_eᵀ x_p,  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)  (edges of a fixed pose: 0)
     double u[4] = {0, 0, 0, 0};
-    if (act && solve) {
-        for (int e = d.lm_off[l] + q; e < d.lm_off[l + 1]; e += kLmLanes) {
-            const int h = d.e_hidx[e];
-            if (h < 0) continue;
-            const double *A = d.A + (size_t)e * 12;
-            const double *Bm = d.B + (size_t)e * 8;
-            double ax0 = 0, ax1 = 0;
+    if (act && solve && !(d.diag & 4)) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const double xk = d.xp[6 * h + k];
-                ax0 += A[k] * xk;
-                ax1 += A[6 + k] * xk;
-            }
+        for (int j = 0; j < kLmSlots; ++j)
+            if (sv[j] && sl[j].h >= 0) lm_hpl_x(sl[j], xs[j], u);
+        for (int e = off0 + q + kLmLanes * kLmSlots; e < off1; e += kLmLanes) {  // long tracks
+            LmEdge s;
+            lm_load_edge(d, e, s);
+            if (s.h < 0) continue;
+            double x[6];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) u[i] += Bm[i] * ax0 + Bm[4 + i] * ax1;
+            for (int k = 0; k < 6; ++k) x[k] = d.xp[6 * s.h + k];
+            lm_hpl_x(s, x, u);
         }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = quad_sum(u[i]);  // all lanes: DPP reads the whole quad
-    double sc = 0.0;
     if (live) {
-        const double *Xc = Xcur(d) + (size_t)l * 4;
-        double *Xt = Xtrial(d) + (size_t)l * 4;
+        double *Xt = d.Xb[cur ^ 1] + (size_t)l * 4;
         if (act) {
             const bool pt = is_point_lm(d, l);
             const int DIM = pt ? 3 : 4;
-            const double lam = d.ctrl->lambda;
             double x[4] = {0, 0, 0, 0};
             if (solve) {
-                double r[4];
+                // (Hll + λI) = L Lᵀ (packed lower), x = L⁻ᵀ L⁻¹ (b_l − u)
+                double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                for (int i = 0; i < 4; ++i) r[i] = d.bl[(size_t)l * 4 + i] - u[i];
-                double L[10], gl[4], y[4] = {0, 0, 0, 0};
-                lm_chol(d, l, lam, L, gl);
+                for (int j = 0; j < 4; ++j) {
+                    if (j < DIM) {
+                        double sj = H[pk(j, j)] + lam;
+#pragma unroll
+                        for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
+                        const double djj = sqrt(sj);
+                        L[pk(j, j)] = djj;
+#pragma unroll
+                        for (int i = j + 1; i < 4; ++i) {
+                            if (i < DIM) {
+                                double t = H[pk(i, j)];
+#pragma unroll
+                                for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
+                                L[pk(i, j)] = t / djj;
+                            }
+                        }
+                    }
+                }
+                double y[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     if (i < DIM) {
-                        double t = r[i];
+                        double t = bl[i] - u[i];
 #pragma unroll
                         for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * y[p];
                         y[i] = t / L[pk(i, i)];
@@ -1670,59 +1769,36 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
             if (q == 0) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    if (i < DIM) sc += x[i] * (lam * x[i] + d.bl[(size_t)l * 4 + i]);
+                    if (i < DIM) sc += x[i] * (lam * x[i] + bl[i]);
             }
-            double X[4], Lp[6];
+            double X[4] = {0, 0, 0, 0}, Lp[6] = {0, 0, 0, 0, 0, 0};
             if (pt) {
                 X[0] = Xc[0] + x[0]; X[1] = Xc[1] + x[1]; X[2] = Xc[2] + x[2]; X[3] = 0.0;
                 if (q == 0) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) Xt[i] = X[i];
                 }
-            } else {
-                const double in[4] = {Xc[0], Xc[1], Xc[2], Xc[3]};
-#if defined(PLBA_DBG_V1)
-                double Lq[6];
-                const double oq = orth_oplus_quad(in, x, q, Lq);
-                orth_oplus(in, x, X);
-                orth_to_pluker(X, Lp);
-                Xt[q] = X[q];
-                if (fabs(oq - X[q]) > 1e-9)
-                    printf("DBG l=%d q=%d in=%.17g %.17g %.17g %.17g x=%.17g %.17g %.17g %.17g oq=%.17g X=%.17g\n", l, q,
-                           in[0], in[1], in[2], in[3], x[0], x[1], x[2], x[3], oq, X[q]);
-#elif defined(PLBA_DBG_V2)
-                orth_oplus(in, x, X);
-                Xt[q] = X[q];
-                (void)orth_oplus_quad(in, x, q, Lp);
-#else
-                Xt[q] = orth_oplus_quad(in, x, q, Lp);
-#endif
+            } else if (!(d.diag & 1)) {
+                Xt[q] = orth_oplus_quad(Xc, x, q, Lp);
             }
-            // the landmark's edges at the trial state (computeActiveErrors of the trial), from
-            // the estimate in registers; lane q takes edges q, q+4, ... (the trial poses were
-            // written by the factorisation kernel)
-            const bool robust = d.ctrl->robust != 0;
+            // the landmark's edges at the trial state (computeActiveErrors of the trial); the
+            // trial poses were written by the factorisation kernel
             const double delta = pt ? d.huber_pt : d.huber_ln;
-            for (int e = d.lm_off[l] + q; e < d.lm_off[l + 1]; e += kLmLanes) {
+            if (!(d.diag & 2))
+#pragma unroll
+            for (int j = 0; j < kLmSlots; ++j)
+                if (sv[j] && sl[j].act) chi += lm_eval(d, sl[j], Ts[j], pt, X, Lp, robust, delta);
+            for (int e = off0 + q + kLmLanes * kLmSlots; e < off1; e += kLmLanes) {  // long tracks
                 if (!d.e_active[e]) continue;
-                const double *T = Ttrial(d) + (size_t)d.e_kf[e] * 12;
-                const double *obs = d.e_obs + (size_t)e * 4;
-                double err[2];
-                if (pt) {
-                    double z;
-                    point_error(T, X, obs, d.cam, err, z);
-                } else {
-                    line_error(T, Lp, obs, d.cam, err);
-                }
-                const double info = d.e_info[e];
-                const double c2 = err[0] * (info * err[0]) + err[1] * (info * err[1]);
-                d.chi2_last[e] = c2;
-                double rho0 = c2, rho1;
-                if (robust) huber(c2, delta, rho0, rho1);
-                chi += rho0;
+                LmEdge s;
+                lm_load_edge(d, e, s);
+                chi += lm_eval(d, s, Tt0 + (size_t)s.kf * 12, pt, X, Lp, robust, delta);
             }
         } else {
-            Xt[q] = Xc[q];
+            if (q == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
+            }
         }
     }
     const double s2 = block_sum<kLmsNT>(sc, sh);
