@@ -118,9 +118,9 @@ def main():
     s.synchronize()
     upload_ms = (time.perf_counter() - t0) * 1e3
 
-    def step():
+    def step(with_trace=True):
         s.reset()
-        return s.lba_plucker(want_outputs=False)
+        return s.lba_plucker(want_outputs=False, with_trace=with_trace)
 
     for _ in range(a.warmup):
         step()
@@ -136,10 +136,11 @@ def main():
     t0 = time.perf_counter()
     iters = 0
     trials = 0
+    trials_per_lba = int(sum(t["trials"] for t in r["trace"]))  # the instrumented step's (same window)
     for _ in range(a.steps):
-        r = step()
+        r = step(with_trace=False)
         iters += int(r["iters"][0] + r["iters"][1])
-        trials += int(sum(t["trials"] for t in r["trace"]))
+        trials += trials_per_lba
     s.synchronize()
     if dist is not None:
         dist.barrier()

@@ -85,6 +85,11 @@ struct plba_ctx {
     // captured step graph (one LM trial + guarded iteration / stage-switch work)
     hipGraph_t step_graph = nullptr;
     hipGraphExec_t step_exec = nullptr;
+    // the same step captured 2, 4, 8, 16 times back to back: a batch of N steps is launched as
+    // its binary decomposition (a graph-to-graph transition costs ~8 us on the device)
+    static constexpr int kMultiLevels = 4;
+    hipGraph_t multi_graph[kMultiLevels] = {};
+    hipGraphExec_t multi_exec[kMultiLevels] = {};
     int last_steps = 16;     // steps the previous schedule needed (first batch size)
     int cur = 0;             // which state buffer holds the current estimate (mirror of Ctrl::cur)
     bool no_graph = false;   // set when the step cannot be captured (RCCL without capture support)
@@ -111,6 +116,12 @@ struct plba_ctx {
         if (step_graph) (void)hipGraphDestroy(step_graph);
         step_exec = nullptr;
         step_graph = nullptr;
+        for (int i = 0; i < kMultiLevels; ++i) {
+            if (multi_exec[i]) (void)hipGraphExecDestroy(multi_exec[i]);
+            if (multi_graph[i]) (void)hipGraphDestroy(multi_graph[i]);
+            multi_exec[i] = nullptr;
+            multi_graph[i] = nullptr;
+        }
         for (void *p : allocs) (void)hipFree(p);
         allocs.clear();
         d = Dev{};
@@ -775,22 +786,44 @@ int launch_step(plba_ctx *ctx) {
     return PLBA_OK;
 }
 
-int capture_step(plba_ctx *ctx) {
-    if (ctx->step_exec) return PLBA_OK;
+int capture_steps(plba_ctx *ctx, int nsteps, hipGraph_t &graph, hipGraphExec_t &exec) {
     const bool t = ctx->timing;
     ctx->timing = false;
     PLBA_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-    int rc = launch_step(ctx);
+    int rc = 0;
+    for (int i = 0; i < nsteps && !rc; ++i) rc = launch_step(ctx);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(ctx->stream, &g);
     ctx->timing = t;
-    if (rc) return rc;
+    if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
     if (e != hipSuccess) {
         ctx->set_error("graph capture failed: %s", hipGetErrorString(e));
         return PLBA_E_DEVICE;
     }
-    ctx->step_graph = g;
-    PLBA_CHECK(hipGraphInstantiate(&ctx->step_exec, g, nullptr, nullptr, 0));
+    graph = g;
+    PLBA_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    return PLBA_OK;
+}
+int capture_step(plba_ctx *ctx) {
+    if (ctx->step_exec) return PLBA_OK;
+    int rc = capture_steps(ctx, 1, ctx->step_graph, ctx->step_exec);
+    for (int i = 0; i < plba_ctx::kMultiLevels && !rc; ++i)
+        rc = capture_steps(ctx, 2 << i, ctx->multi_graph[i], ctx->multi_exec[i]);
+    return rc;
+}
+// launch n replays of the step as the binary decomposition of n over the captured graphs
+int launch_steps_graph(plba_ctx *ctx, int n) {
+    constexpr int L = plba_ctx::kMultiLevels;
+    while (n >= (2 << (L - 1))) {
+        PLBA_CHECK(hipGraphLaunch(ctx->multi_exec[L - 1], ctx->stream));
+        n -= 2 << (L - 1);
+    }
+    for (int i = L - 1; i >= 0; --i)
+        if (n & (2 << i)) PLBA_CHECK(hipGraphLaunch(ctx->multi_exec[i], ctx->stream));
+    if (n & 1) PLBA_CHECK(hipGraphLaunch(ctx->step_exec, ctx->stream));
     return PLBA_OK;
 }
 
@@ -825,9 +858,11 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     int batch = std::max(4, ctx->last_steps);
     const int max_steps = init.n_stages * 10 * (init.max_iters[0] + init.max_iters[1] + 2) + 8;
     for (;;) {
-        for (int b = 0; b < batch; ++b) {
-            if (use_graph) PLBA_CHECK(hipGraphLaunch(ctx->step_exec, ctx->stream));
-            else {
+        if (use_graph) {
+            int rc = launch_steps_graph(ctx, batch);
+            if (rc) return rc;
+        } else {
+            for (int b = 0; b < batch; ++b) {
                 int rc = launch_step(ctx);
                 if (rc) return rc;
             }

@@ -150,6 +150,9 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #else
 #pragma unroll
                 for (int q = 0; q < 36; ++q) a1[q] = pA[s1 * 36 + q];
+                // keep these loads in front of the Gauss–Jordan so their latency hides behind it
+                // (the scheduler would otherwise sink them to their use in E/F)
+                __builtin_amdgcn_sched_barrier(0);
 #endif
                 STAMP(0);
                 // B: Gauss–Jordan on block row k across the lanes (pivot lanes 6*sk + p)

@@ -209,7 +209,7 @@ class Solver:
         self._check(self.L.plba_download(self.ctx, _p(T), _p(P), _p(O)), "plba_download")
         return T, P, O
 
-    def lba_plucker(self, want_outputs: bool = True) -> dict:
+    def lba_plucker(self, want_outputs: bool = True, with_trace: bool = True) -> dict:
         """Full two-stage schedule (src/mapHandler.cpp:6119-6160) on the uploaded window."""
         g = self.graph
         if want_outputs:
@@ -221,7 +221,8 @@ class Solver:
             self._check(self.L.plba_lba_plucker(self.ctx, C.byref(r)), "plba_lba_plucker")
             out = dict(iters=np.array([r.iters[0], r.iters[1]]), chi2=np.array([r.chi2[0], r.chi2[1]]),
                        solve_ms=r.solve_ms)
-        out["trace"] = self.trace()
+        if with_trace:
+            out["trace"] = self.trace()
         return out
 
     def trace(self) -> np.ndarray:
