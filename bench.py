@@ -167,6 +167,8 @@ def main():
         prof_name = name
         if name == "k_rcs_factor" and info.get("banded"):
             prof_name = "k_rcs_factor_twisted" if info.get("twisted") else "k_rcs_factor_band"
+            if info.get("column_lane"):
+                prof_name += "_cl"
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
         traffic = None
         if os.path.exists(pmc_path):
@@ -220,9 +222,10 @@ def main():
                 "alg_bytes_per_launch": alg,
                 "avg_launch_us": avg_ms * 1e3,
                 "launches_per_lba": nl,
-                "note": ("latency-bound banded LDLᵀ of the reduced camera system (a serial chain of 6x6 "
-                         "block pivots, two-sided on 2 workgroups) + pose update; bytes/launch are tiny by "
-                         "nature — see DESIGN.md §4"),
+                "note": ("latency-bound banded LDLᵀ of the reduced camera system: a serial chain of 6x6 "
+                         "block pivots (column-lane Gauss–Jordan on one wave per segment, two segments "
+                         "meeting at a separator) + back substitution + pose update; bytes/launch are tiny "
+                         "by nature — see DESIGN.md §4"),
             },
             "iteration_roofline": {
                 "alg_bytes_per_iter": iter_bytes,

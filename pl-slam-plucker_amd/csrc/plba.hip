@@ -591,6 +591,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.X_init, X);
     UPLOAD(d.Xb[0], X);
     ALLOC(d.Xb[1], X.size());
+    ALLOC(d.Lpb[0], (size_t)std::max(n_ln, 1) * 8);
+    ALLOC(d.Lpb[1], (size_t)std::max(n_ln, 1) * 8);
     UPLOAD(d.kf_hidx, kf_hidx);
     UPLOAD(d.e_lm, e_lm);
     UPLOAD(d.e_kf, e_kf);
@@ -839,6 +841,10 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     Dev &d = ctx->d;
     *ctx->h_ctrl = init;
     PLBA_CHECK(hipMemcpyAsync(d.ctrl, ctx->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, ctx->stream));
+    if (d.n_ln > 0) {  // Plücker vectors of the current line states (read by k_linearize)
+        hipLaunchKernelGGL(k_line_pluker, dim3(blocks_for(d.n_ln)), dim3(kBlock), 0, ctx->stream, d);
+        PLBA_CHECK(hipGetLastError());
+    }
     // the host transport synchronises inside the step: no graph then
     bool use_graph = !ctx->timing && ctx->comm.kind != plba_ctx::Comm::HOST && !ctx->no_graph;
     if (use_graph) {

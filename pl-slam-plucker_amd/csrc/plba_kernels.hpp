@@ -78,6 +78,8 @@ struct Dev {
     // flips ctrl->cur (g2o's push/pop/discardTop without a copy)
     double *Tb[2], *T_init;             // [n_kf][12]
     double *Xb[2], *X_init;             // [n_lm][4]
+    double *Lpb[2];                     // [n_ln][8]: Plücker vector (6) of each line at Xb[i]
+                                        //   (k_line_pluker at schedule start, then k_lm_solve)
     int32_t *kf_hidx;                   // [n_kf]
     // edges, landmark-major CSR order (points first, then lines)
     int32_t *e_lm, *e_kf, *e_hidx;      // [E]
@@ -269,8 +271,11 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
                 Jl[7] = 0; Jl[6] = Jl[5]; Jl[5] = Jl[4]; Jl[4] = Jl[3]; Jl[3] = 0;
                 delta = d.huber_pt;
             } else {
+                // changeOrthToPluker of the current state, evaluated once per line (Lpb)
+                const double *Lc = d.Lpb[cc->cur] + (size_t)(lm - d.n_pt) * 8;
                 double L[6];
-                orth_to_pluker(X, L);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) L[k] = Lc[k];
                 line_jac(T, X, L, obs, d.cam, d.corrected, err, Jl, Jp);
                 delta = d.huber_ln;
             }
@@ -1780,6 +1785,11 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
                 }
             } else if (!(d.diag & 1)) {
                 Xt[q] = orth_oplus_quad(Xc, x, q, Lp);
+                if (q == 0) {
+                    double *Lt = d.Lpb[cur ^ 1] + (size_t)(l - d.n_pt) * 8;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) Lt[k] = Lp[k];
+                }
             }
             // the landmark's edges at the trial state (computeActiveErrors of the trial); the
             // trial poses were written by the factorisation kernel
@@ -1798,6 +1808,12 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
             if (q == 0) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
+                if (!is_point_lm(d, l)) {  // an inactive line keeps its Plücker vector too
+                    const double *Lc = d.Lpb[cur] + (size_t)(l - d.n_pt) * 8;
+                    double *Lt = d.Lpb[cur ^ 1] + (size_t)(l - d.n_pt) * 8;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) Lt[k] = Lc[k];
+                }
             }
         }
     }
@@ -1882,6 +1898,19 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
     } else {
         c->need_iter = 1;
     }
+}
+
+// changeOrthToPluker (g2o_types.h:367-387) of every line at the current state into Lpb[cur];
+// launched once per schedule (estimates may have been reset or uploaded in between)
+__global__ void k_line_pluker(Dev d) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= d.n_ln) return;
+    const int cur = d.ctrl->cur;
+    double L[6];
+    orth_to_pluker(d.Xb[cur] + (size_t)(d.n_pt + l) * 4, L);
+    double *o = d.Lpb[cur] + (size_t)l * 8;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o[k] = L[k];
 }
 
 // ---------------------------------------------------------------- outlier pass helpers

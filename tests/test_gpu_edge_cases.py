@@ -124,6 +124,29 @@ def test_twisted_factorisation_matches_single_sweep(solver, monkeypatch, cfg, kw
     assert np.abs(tw["kf_Tcw"] - one["kf_Tcw"]).max() < 1e-10
 
 
+@pytest.mark.parametrize("tmax", [2, 3, 5, 8, 10])
+@pytest.mark.parametrize("n_kf", [14, 48])
+def test_column_lane_factorisation_bandwidths(solver, monkeypatch, tmax, n_kf):
+    # column-lane band LDLᵀ (plba_band_cl.hpp) at bandwidths 1..9, single sweep (14 KF) and
+    # two-sided (48 KF, bw <= 9 -> nf >= 2bw + 16), vs the oracle and vs the 16-wave kernel
+    g = synth.generate("C1L", n_kf=n_kf, n_pt=30 * n_kf, n_ln=6 * n_kf, seed=300 + tmax + n_kf,
+                       track_min=2, track_max=tmax, fixed_frac=0.1)
+    ref = oa.lba_plucker(g)
+    solver.upload(g)
+    st = solver.structure_stats()
+    assert st["banded"] == 1 and st["column_lane"] == 1 and st["bw"] <= 9, st
+    assert st["twisted"] == (1 if st["nf"] >= 2 * st["bw"] + 16 else 0), st
+    cl = solver.lba_plucker()
+    _check(cl, ref)
+    monkeypatch.setenv("PLBA_NO_CL", "1")
+    solver.upload(g)
+    assert solver.structure_stats()["column_lane"] == 0
+    old = solver.lba_plucker()
+    monkeypatch.delenv("PLBA_NO_CL")
+    _check(old, ref)
+    assert np.abs(cl["kf_Tcw"] - old["kf_Tcw"]).max() < 1e-9
+
+
 def test_empty_graph(solver):
     g = synth.generate("C1", n_pt=0, n_ln=0)
     out, ref = _run(solver, g)
