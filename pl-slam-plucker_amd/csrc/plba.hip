@@ -130,13 +130,18 @@ struct plba_ctx {
     template <typename T>
     int alloc(T *&p, size_t count) {
         p = nullptr;
-        if (count == 0) count = 1;
+        // at least 128 bytes, zero-filled when the array is (nearly) empty: kernels issue
+        // unconditional loads of one record (an edge's 12 A doubles, a pose's 6 x_p doubles)
+        // for dead lanes, which must stay inside the allocation and read defined indices
+        const bool tiny = count * sizeof(T) < 128;
+        if (tiny) count = (128 + sizeof(T) - 1) / sizeof(T);
         hipError_t e = hipMalloc((void **)&p, count * sizeof(T));
         if (e != hipSuccess) {
             set_error("hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
             return PLBA_E_NOMEM;
         }
         allocs.push_back(p);
+        if (tiny) (void)hipMemset(p, 0, count * sizeof(T));
         if constexpr (std::is_same<T, double>::value) {
             // PLBA_POISON=1 (diagnostics only): fill f64 buffers with NaN to expose reads of
             // memory no kernel wrote (a reused allocation is not zero).
@@ -610,16 +615,18 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.B, (size_t)E * 8);
     ALLOC(d.chi2_last, E);
     // Hpp | b_p | χ² | active | landmark max per rank: one array, all-reduced when sharded
-    ALLOC(d.red_iter, (size_t)nf * 42 + 2 + R);
+    ALLOC(d.red_iter, (size_t)nf * 43 + 2 + R);
     d.Hpp = d.red_iter;
     d.bp = d.red_iter + (size_t)nf * 36;
+    d.pact = d.red_iter + (size_t)nf * 42;
     if (sharded) {
-        ALLOC(d.red_iter_loc, (size_t)nf * 42 + 2 + R);
+        ALLOC(d.red_iter_loc, (size_t)nf * 43 + 2 + R);
     } else {
         d.red_iter_loc = d.red_iter;
     }
     d.Hpp_w = d.red_iter_loc;
     d.bp_w = d.red_iter_loc + (size_t)nf * 36;
+    d.pact_w = d.red_iter_loc + (size_t)nf * 42;
     ALLOC(d.Hll, (size_t)n_lm * 10);
     ALLOC(d.bl, (size_t)n_lm * 4);
     ALLOC(d.Z, (size_t)E * 8);
@@ -658,7 +665,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_chi2, d.n_lin_blocks);
     ALLOC(d.part_any, d.n_lm_blocks);
     ALLOC(d.part_max, nf + d.n_lm_blocks);
-    ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * 27);
+    ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * kPP);
     ALLOC(d.part_lm, std::max(d.n_lms_blocks, 1));
     ALLOC(d.part_lms, d.n_lms_blocks);
     ALLOC(d.part_ps, d.n_kf_blocks);
@@ -684,6 +691,10 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 #undef UPLOAD
     if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)band_lds_bytes(bw, nf)));
+    if (d.cl) {  // the column-lane kernel's LDS grows with nf (x_p staging of the two-sided variant)
+        const void *k = cl_kernel_impl(bw, twisted, std::make_integer_sequence<int, kClMaxBW + 1>{});
+        PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, twisted)));
+    }
     if (twisted) {
         PLBA_CHECK(hipFuncSetAttribute(twisted_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)twisted_lds_bytes(bw, nf)));
@@ -758,7 +769,7 @@ int launch_step(plba_ctx *ctx) {
     }
     if (d.sharded) {
         LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kInitNT), 0, s, d));
-        COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 42 + 2 + d.nranks);
+        COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 43 + 2 + d.nranks);
     }
     LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kInitNT), 0, s, d));
     if (d.n_lm > 0) {
@@ -1039,7 +1050,12 @@ int plba_set_edge_levels(plba_ctx *ctx, const uint8_t *ept_level, const uint8_t 
         lv[e] = is_pt ? (ept_level ? ept_level[o] : 0) : (eln_level ? eln_level[o] : 0);
     }
     ctx->h_level = lv;
-    if (E) PLBA_CHECK(hipMemcpy(ctx->d.e_level, lv.data(), E, hipMemcpyHostToDevice));
+    // on the solver stream (ordered after a pending plba_reset_estimates memset), then wait:
+    // lv is a local buffer
+    if (E) {
+        PLBA_CHECK(hipMemcpyAsync(ctx->d.e_level, lv.data(), E, hipMemcpyHostToDevice, ctx->stream));
+        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    }
     ctx->initialized = false;
     return PLBA_OK;
 }

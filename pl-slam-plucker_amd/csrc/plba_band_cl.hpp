@@ -332,23 +332,25 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_band_cl(Dev d) {
     }
 }
 
-// Two-sided variant. Workgroup 1 eliminates the block-reversed bottom segment (rows nf-1 ..
-// m+bw) and publishes its separator window; workgroup 0 eliminates rows 0..m-1, waits for it,
-// adds the bottom segment's Schur contribution (W1 - A_sep) to its own window and simply keeps
-// eliminating the bw separator rows as ordinary band steps (the separator is itself a band of
-// width bw), so no dense separator solve is needed. Back substitution: the separator rows first
-// (one wave), then both segments concurrently on two waves.
+// Two-sided variant. Workgroup 0 eliminates the top segment (rows 0..m-1), workgroup 1 the
+// block-reversed bottom segment (rows nf-1 .. m+bw); each publishes its separator window and its
+// L / z rows. The workgroup that arrives second (last-arriver counter, no spin: MI355X_MICROARCH.md
+// hand-off "counter form") takes over: it puts segment 0's separator window into its LDS window
+// (already there when it is workgroup 0), adds the bottom segment's Schur contribution
+// W1 - A_sep and keeps eliminating the bw separator rows as ordinary band steps (the separator
+// is itself a band of width bw), so no dense separator solve is needed. Back substitution: the
+// separator rows first (one wave), then both segments concurrently on two waves.
 template <int BW>
 __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d) {
     TRIAL_GUARD
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    __shared__ int s_fail;
+    __shared__ int s_fail, s_last;
     if constexpr (BW >= 1 && BW <= kClMaxBW) {
         constexpr int W = BW + 1;
         const int seg = blockIdx.x, tid = threadIdx.x;
         const int m = d.tw_m, n1 = d.nf - BW - d.tw_m;
         const size_t sep_stride = (size_t)BW * W * 36 + (size_t)BW * 6;
-        double *sep1 = d.tw_sep + sep_stride;
+        double *sep0 = d.tw_sep, *sep1 = d.tw_sep + sep_stride;
         bool fail = false;
 #ifdef PLBA_STAMPS
         unsigned long long t0 = __builtin_readcyclecounter();
@@ -361,37 +363,45 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d) {
 #else
 #define CL_MARK(q) do {} while (0)
 #endif
-        if (seg == 1) {
-            const BandSeg g{d.Bd2, d.bs2, d.Lband2, nullptr, d.zb2, n1 + BW, n1, nullptr};
-            cl_forward<BW>(g, 0, n1, true, lds, fail);
-            CL_MARK(1);
-            cl_store_sep<BW>(lds, n1, sep1);
-            // hand-off (MI355X_MICROARCH.md, workgroup hand-off): drain every wave's stores,
-            // one agent-scope release, then the flag
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) {
-                __hip_atomic_store(&d.tw_fail[1], fail ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_fetch_add(d.tw_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            return;
-        }
-        const BandSeg g{d.Bd, d.bs, d.Lband, nullptr, d.zb, m + BW, m, nullptr};
-        cl_forward<BW>(g, 0, m, true, lds, fail, d.stamps);
-        CL_MARK(0);
-        // wait for segment 1 (bounded: a missing partner fails the solve instead of hanging)
+        const BandSeg g = seg == 0 ? BandSeg{d.Bd, d.bs, d.Lband, nullptr, d.zb, m + BW, m, nullptr}
+                                   : BandSeg{d.Bd2, d.bs2, d.Lband2, nullptr, d.zb2, n1 + BW, n1, nullptr};
+        const int mine = seg == 0 ? m : n1;
+        cl_forward<BW>(g, 0, mine, true, lds, fail, seg == 0 ? d.stamps : nullptr);
+        CL_MARK(seg);
+        cl_store_sep<BW>(lds, mine, seg == 0 ? sep0 : sep1);
+        // hand-off: every wave drains its L / z / separator stores, one agent release by lane 0,
+        // then the arrival counter; the workgroup whose add returns 1 is last and acquires once
+        // before reading the other's data. Exactly two arrivals per launch (both workgroups pass
+        // or both skip TRIAL_GUARD), so the last arriver resets the counter for the next launch.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         if (tid == 0) {
-            int spins = 0, got = 0;
-            while (!(got = __hip_atomic_load(d.tw_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) && spins < (1 << 22)) {
-                __builtin_amdgcn_s_sleep(2);
-                ++spins;
+            __hip_atomic_store(&d.tw_fail[seg], fail ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int old = __hip_atomic_fetch_add(d.tw_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old == 1 ? 1 : 0;
+            if (old == 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(d.tw_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+                s_fail = (__hip_atomic_load(&d.tw_fail[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                          __hip_atomic_load(&d.tw_fail[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? 1 : 0;
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __hip_atomic_store(d.tw_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-            const int f1 = __hip_atomic_load(&d.tw_fail[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_fail = (!got || f1 || fail) ? 1 : 0;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        const BandSeg g0{d.Bd, d.bs, d.Lband, nullptr, d.zb, m + BW, m, nullptr};
+        if (seg == 1) {  // segment 0's separator window (rows m..m+bw-1) into this LDS window
+            double *win = lds, *bwin = win + (BW + 2) * W * 36;
+            for (int t = tid; t < (BW + 2) * W * 36; t += kClNT) {
+                const int i = t / (W * 36), rem = t % (W * 36);
+                win[((m + i) % (BW + 2)) * W * 36 + rem] = i < BW ? sep0[t] : 0.0;
+            }
+            for (int t = tid; t < (BW + 2) * 6; t += kClNT) {
+                const int i = t / 6;
+                bwin[((m + i) % (BW + 2)) * 6 + t % 6] = i < BW ? sep0[(size_t)BW * W * 36 + t] : 0.0;
+            }
         }
         __syncthreads();
         // separator rows m+i: + (W1 - A_sep), W1 given in segment 1's reversed numbering
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d) {
         __syncthreads();
         CL_MARK(2);
         bool fail2 = false;
-        cl_forward<BW>(g, m, m + BW, false, lds, fail2);
+        cl_forward<BW>(g0, m, m + BW, false, lds, fail2);
         CL_MARK(3);
         if (tid == 0) {
             if (fail2) s_fail = 1;

@@ -127,11 +127,12 @@ struct Dev {
     int32_t n_lm_g, E_g;                // whole-window landmark / edge counts
     // Out-of-place (send *_loc -> receive) so that replaying a step whose kernels were guarded
     // off re-reduces unchanged partials and leaves the totals intact.
-    double *red_iter, *red_iter_loc;    // [nf*42 + 2 + nranks]: Hpp | b_p | χ² | active | lm max per rank
+    double *red_iter, *red_iter_loc;    // [nf*43 + 2 + nranks]: Hpp | b_p | #active edges | χ² | active | lm max per rank
     double *red_rcs, *red_rcs_loc;      // [nblk*36 + nf*6]: Σ A₁ᵀZ₁Z₂ᵀA₂ per block | Σ A_eᵀq_e per pose
     double *red_dec, *red_dec_loc;      // [2]: trial χ² | landmark part of Σx(λx+b)
     double *Hpp_w, *bp_w;               // where pose_combine writes (== Hpp, bp unless sharded)
-    double *pose_part;                  // [nf][kPoseParts][27] partial Σ AᵀA (upper), Σ Aᵀc
+    double *pose_part;                  // [nf][kPoseParts][kPP] partial Σ AᵀA (upper), Σ Aᵀc, #active edges
+    double *pact, *pact_w;              // [nf] active edges of each free pose (0 = vertex inactive in g2o)
     int32_t *lm_gpos, *e_gpos;          // local landmark / edge -> whole-window position
     double *gat;                        // [n_lm_g*4 + 3*E_g] final gather buffer
     // two-sided banded factorisation (k_rcs_factor_twisted)
@@ -308,21 +309,22 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
 // The iteration's two reductions in ONE launch of 64-thread workgroups (they are independent
 // and each alone leaves most of the chip idle):
 //   workgroups [0, kPoseParts·nf): pose h, part j sums A_eᵀA_e and A_eᵀc_e over the pose's
-//     edges p ≡ 64j + lane (mod 64·kPoseParts) into pose_part[h][j][27]; the parts are added in
+//     edges p ≡ 64j + lane (mod 64·kPoseParts) into pose_part[h][j][kPP]; the parts are added in
 //     j order by pose_combine (k_iter_init / k_iter_pack) — the same per-lane sets and order
 //     as one 256-thread workgroup per pose, so the sums are deterministic;
 //   workgroups [kPoseParts·nf, ...): 64 landmarks each, Hll = Σ B_eᵀB_e, b_l = Σ B_eᵀc_e
 //     (and, on a stage switch, the landmark activation).
 constexpr int kPoseParts = 4;
+constexpr int kPP = 28;        // per pose part: 21 (upper Σ AᵀA) + 6 (Σ Aᵀc) + active-edge count
 constexpr int kInitNT = 1024;  // k_iter_init / k_iter_pack: one wide workgroup (the pose combine)
 
 // packed lower-triangular index for 4x4 symmetric
 __device__ __forceinline__ constexpr int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
 __device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
-    double acc[27];
+    double acc[kPP];
 #pragma unroll
-    for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+    for (int k = 0; k < kPP; ++k) acc[k] = 0.0;
     // kU edges per pass with all their loads issued before the arithmetic (the per-thread
     // chains are edge-index -> A/c misses; one edge at a time leaves them serialised)
     constexpr int S = kPoseParts * 64, kU = 4;
@@ -344,6 +346,7 @@ __device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
 #pragma unroll
         for (int j = 0; j < kU; ++j) {
             if (ei[j] < 0) break;
+            acc[27] += d.e_active[ei[j]] ? 1.0 : 0.0;
             const double *a0 = a[j], *a1 = a[j] + 6;
             int idx = 0;
 #pragma unroll
@@ -355,11 +358,11 @@ __device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
         }
     }
 #pragma unroll
-    for (int k = 0; k < 27; ++k) acc[k] = wave_sum(acc[k]);
+    for (int k = 0; k < kPP; ++k) acc[k] = wave_sum(acc[k]);
     if (threadIdx.x == 0) {
-        double *o = d.pose_part + ((size_t)h * kPoseParts + part) * 27;
+        double *o = d.pose_part + ((size_t)h * kPoseParts + part) * kPP;
 #pragma unroll
-        for (int k = 0; k < 27; ++k) o[k] = acc[k];
+        for (int k = 0; k < kPP; ++k) o[k] = acc[k];
     }
 }
 
@@ -429,12 +432,12 @@ __global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
 template <int NT>
 __device__ __forceinline__ double pose_combine(const Dev &d, double *H, double *bp) {
     double m = 0.0;
-    for (int i = threadIdx.x; i < d.nf * 27; i += NT) {
-        const int h = i / 27, k = i % 27;
-        const double *src = d.pose_part + (size_t)h * kPoseParts * 27 + k;
+    for (int i = threadIdx.x; i < d.nf * kPP; i += NT) {
+        const int h = i / kPP, k = i % kPP;
+        const double *src = d.pose_part + (size_t)h * kPoseParts * kPP + k;
         double v = src[0];
 #pragma unroll
-        for (int j = 1; j < kPoseParts; ++j) v += src[j * 27];
+        for (int j = 1; j < kPoseParts; ++j) v += src[j * kPP];
         if (k < 21) {
             int r = 0, rem = k;
             while (rem >= 6 - r) { rem -= 6 - r; ++r; }
@@ -442,8 +445,10 @@ __device__ __forceinline__ double pose_combine(const Dev &d, double *H, double *
             H[(size_t)h * 36 + r * 6 + cc] = v;
             H[(size_t)h * 36 + cc * 6 + r] = v;
             if (r == cc) m = fmax(m, fabs(v));
-        } else {
+        } else if (k < 27) {
             bp[(size_t)h * 6 + (k - 21)] = v;
+        } else {
+            d.pact_w[h] = v;
         }
     }
     return m;
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(kInitNT) void k_iter_pack(Dev d) {
     int any = 0;
     for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) any |= d.part_any[i];
     any = __syncthreads_or(any);
-    double *o = d.red_iter_loc + (size_t)d.nf * 42;
+    double *o = d.red_iter_loc + (size_t)d.nf * 43;
     if (threadIdx.x == 0) {
         o[0] = chi;
         o[1] = any ? 1.0 : 0.0;
@@ -479,7 +484,7 @@ __global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
     double chi, mx;
     bool any;
     if (d.sharded) {  // totals from the all-reduced iteration array
-        const double *o = d.red_iter + (size_t)d.nf * 42;
+        const double *o = d.red_iter + (size_t)d.nf * 43;
         double m = 0.0;
         for (int i = threadIdx.x; i < d.nf * 6; i += kInitNT) m = fmax(m, fabs(d.Hpp[(i / 6) * 36 + (i % 6) * 7]));
         for (int r = threadIdx.x; r < d.nranks; r += kInitNT) m = fmax(m, o[2 + r]);
@@ -635,7 +640,10 @@ __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
     const int r = e / 6, c = e % 6;
     if (diag) {
         double h = d.Hpp[(size_t)i1 * 36 + e] - sacc;
-        if (r == c) h += d.ctrl->lambda;
+        // a free pose with no active edge is not in g2o's system (SparseOptimizer activation,
+        // SURVEY.md §8 A13); its all-zero block row becomes I (x = 0 exactly) instead of λI,
+        // which would be a zero pivot at λ = 0
+        if (r == c) h += d.pact[i1] != 0.0 ? d.ctrl->lambda : 1.0;
         if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
         else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
         if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1)) * 36 + e] = h;

@@ -113,13 +113,17 @@ class Solver:
     """One plba context bound to a device (g2o::SparseOptimizer equivalent)."""
 
     def __init__(self, device: int = 0, corrected_line_jacobian: bool = False, verbose: bool = False,
-                 kernel_timing: bool = False):
+                 kernel_timing: bool = False, tau: Optional[float] = None, max_trials: Optional[int] = None):
         self.L = load()
         o = capi.PlbaOpts()
         self.L.plba_default_opts(C.byref(o))
         o.device = device
         o.corrected_line_jacobian = int(corrected_line_jacobian)
         o.verbose = int(verbose)
+        if tau is not None:
+            o.tau = float(tau)          # OptimizationAlgorithmLevenberg τ (λ init = τ·max|H_jj|)
+        if max_trials is not None:
+            o.max_trials = int(max_trials)
         self.ctx = C.c_void_p()
         rc = self.L.plba_create(C.byref(self.ctx), C.byref(o))
         if rc != 0:

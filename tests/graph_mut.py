@@ -75,3 +75,15 @@ def fixed_only_landmarks(g: Graph) -> Graph:
     sel = g.ept_lm < 20
     h.ept_kf = np.where(sel, fixed[np.arange(g.n_ept) % len(fixed)], g.ept_kf).astype(np.int32)
     return h
+
+
+def zero_information_keyframe(g: Graph) -> Graph:
+    """Ω = 0 on every edge of one free keyframe: the vertex stays active (it has edges) but its
+    reduced-camera block row is exactly zero, so with λ = 0 the LDLᵀ meets an exact zero pivot
+    in any elimination order (g2o's LinearSolverEigen fails there too)."""
+    h = g.copy()
+    free = np.nonzero(g.kf_fixed == 0)[0]
+    k = free[len(free) // 2]
+    h.ept_info = np.where(g.ept_kf == k, 0.0, g.ept_info)
+    h.eln_info = np.where(g.eln_kf == k, 0.0, g.eln_info)
+    return h

@@ -169,37 +169,131 @@ def test_corrected_line_jacobian_option():
 
 
 def test_g2o_style_call_sequence(solver):
-    """setRobustKernel / initializeOptimization(0) / optimize(5) as separate calls equals the
-    oracle's stage 1 (src/mapHandler.cpp:6121-6122)."""
+    """The reference's call sequence as separate g2o-style calls (src/mapHandler.cpp:6119-6160):
+    setRobustKernel(Huber) / initializeOptimization(0) / optimize(5), classification on the host
+    from chi2() / isDepthPositive(), setLevel(1), setRobustKernel(0), initializeOptimization(0) /
+    optimize(10), computeError() of the level-1 edges, chi2() — equals the oracle's schedule."""
     g = synth.generate("C1L")
-    ref = oa.lba_plucker(g, stage_iters=(5, 0))
+    ref1 = oa.lba_plucker(g, stage_iters=(5, 0))
+    ref = oa.lba_plucker(g)
     solver.upload(g)
     solver.set_robust(True)
     solver.initialize_optimization(0)
     it, chi = solver.optimize(5)
-    assert it == ref["iters"][0]
-    assert abs(chi - ref["chi2"][0]) <= 1e-6 * ref["chi2"][0]
+    assert it == ref1["iters"][0]
+    assert abs(chi - ref1["chi2"][0]) <= 1e-6 * ref1["chi2"][0]
     T, P, O = solver.download()
-    assert _amax(P - ref["pt_xyz"]) <= EST_RTOL * _amax(ref["pt_xyz"])
-    assert _amax(O - ref["ln_orth"]) <= EST_RTOL * max(_amax(ref["ln_orth"]), 1.0)
+    assert _amax(P - ref1["pt_xyz"]) <= EST_RTOL * _amax(ref1["pt_xyz"])
+    assert _amax(O - ref1["ln_orth"]) <= EST_RTOL * max(_amax(ref1["ln_orth"]), 1.0)
     # per-edge chi2 after optimize() follows g2o's last-evaluated semantics
     pc, pd, lc = solver.edge_chi2()
-    np.testing.assert_allclose(pc[ref["ept_level"] == 0], ref["ept_chi2"][ref["ept_level"] == 0], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pc, ref1["ept_chi2"], rtol=1e-6, atol=1e-9)
+    # classification (src/mapHandler.cpp:6125-6147) on the host, then stage 2 through the C ABI
+    pl = ((pc > 5.991) | (pd == 0)).astype(np.uint8)
+    ll = (lc > 5.991).astype(np.uint8)
+    np.testing.assert_array_equal(pl, ref["ept_level"])
+    np.testing.assert_array_equal(ll, ref["eln_level"])
+    solver.set_edge_levels(pl, ll)
+    solver.set_robust(False)
+    solver.initialize_optimization(0)
+    it2, chi2 = solver.optimize(10)
+    assert it2 == ref["iters"][1]
+    assert abs(chi2 - ref["chi2"][1]) <= 1e-6 * ref["chi2"][1]
+    solver.refresh_edge_errors(1)
+    pc2, pd2, lc2 = solver.edge_chi2()
+    np.testing.assert_allclose(pc2, ref["ept_chi2"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(lc2, ref["eln_chi2"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_array_equal(pd2, ref["ept_depth_ok"])
+    T2, P2, O2 = solver.download()
+    assert _amax(T2 - ref["kf_Tcw"]) <= EST_RTOL * _amax(ref["kf_Tcw"])
+    assert _amax(P2 - ref["pt_xyz"]) <= EST_RTOL * _amax(ref["pt_xyz"])
+    assert _amax(O2 - ref["ln_orth"]) <= EST_RTOL * max(_amax(ref["ln_orth"]), 1.0)
 
 
-def test_two_contexts_in_one_process():
+def test_set_edge_levels_after_reset_is_ordered(solver):
+    """plba_set_edge_levels right after plba_reset_estimates (whose level memset is queued on the
+    solver stream): the levels must land after the reset, so stage 2 sees them."""
+    g = synth.generate("C1L")
+    ref = oa.lba_plucker(g)
+    solver.upload(g)
+    for _ in range(3):
+        solver.reset()
+        solver.set_edge_levels(ref["ept_level"], ref["eln_level"])
+        solver.set_robust(False)
+        solver.initialize_optimization(1)   # only the level-1 edges: non-empty iff the levels landed
+        it, _ = solver.optimize(1)
+        assert it == 1
+
+
+def test_zero_pivot_rejects_every_trial():
+    """LinearSolverEigen fails iff an LDLᵀ pivot is exactly 0: with τ = 0
+    (λ = 0) a free keyframe whose edges all carry Ω = 0 stays active but leaves an exactly zero
+    6x6 block on the reduced camera diagonal, so every solve of the Huber stage fails, every
+    trial is rejected with the previous x (g2o still calls update), and optimize(5) stops after
+    maxTrials with Terminate — the same path as the oracle's stage 1."""
     from plba.lib import Solver
-    g1, g2 = synth.generate("C1"), synth.generate("C1L")
-    with Solver() as a, Solver() as b:
-        a.upload(g1)
-        b.upload(g2)
-        oa_, ob_ = a.lba_plucker(), b.lba_plucker()
-    _check(oa_, oa.lba_plucker(g1))
-    _check(ob_, oa.lba_plucker(g2))
+    g = gm.zero_information_keyframe(synth.generate("C1L", track_min=3, seed=41))
+    ref = oa.lba_plucker(g, tau=0.0, stage_iters=(5, 0))
+    tr_ref = ref["trace"]
+    assert len(tr_ref) == 1 and tr_ref[0]["trials"] == 10 and tr_ref[0]["result"] == 1, tr_ref
+    with Solver(tau=0.0) as s:
+        s.upload(g)
+        s.set_robust(True)
+        s.initialize_optimization(0)
+        it, chi = s.optimize(5)
+        tr = s.trace()
+        T, P, O = s.download()
+    assert it == ref["iters"][0] == 1
+    assert len(tr) == 1 and tr[0]["trials"] == 10 and tr[0]["result"] == 1, tr
+    assert tr[0]["lambda_start"] == 0.0 and tr[0]["lambda_end"] == 0.0
+    assert abs(chi - ref["chi2"][0]) <= 1e-9 * ref["chi2"][0]
+    # nothing moved: every trial was popped
+    np.testing.assert_array_equal(T, g.kf_Tcw)
+    np.testing.assert_array_equal(P, g.pt_xyz)
+    np.testing.assert_array_equal(O, g.ln_orth)
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("cfg", ["C3", "C4"])
+@pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
 def test_large_configs_match_oracle(solver, cfg):
     g = synth.generate(cfg)
     _check(*_run(solver, g))
+
+
+def test_idle_free_pose_is_inactive_at_zero_lambda():
+    """A free keyframe with no edge is not an active vertex in g2o, so it is not in the linear
+    system at all: even at λ = 0 (τ = 0) it must not make the solve fail (its block is I, x = 0),
+    and the solve must be the one of the same window without it. (At λ = 0 the Huber stage is a
+    Gauss–Newton step on a barely conditioned system, so the comparison is GPU vs GPU; the oracle
+    agrees on the trial count and on the pose staying put.)"""
+    from plba.lib import Solver
+    base = synth.generate("C1L", track_min=3, seed=41)
+    g = gm.add_idle_free_pose(base)
+    ref = oa.lba_plucker(g, tau=0.0, stage_iters=(5, 0))
+    res = []
+    for h in (g, base):
+        with Solver(tau=0.0) as s:
+            s.upload(h)
+            s.set_robust(True)
+            s.initialize_optimization(0)
+            it, chi = s.optimize(5)
+            tr = s.trace()
+            T, P, O = s.download()
+        res.append((it, chi, tr, T, P, O))
+    (it, chi, tr, T, P, O), (it0, chi0, tr0, T0, P0, O0) = res
+    assert it == it0 == ref["iters"][0]
+    assert [int(t["trials"]) for t in tr] == [int(t["trials"]) for t in tr0] == [int(t["trials"]) for t in ref["trace"]]
+    assert abs(chi - chi0) <= 1e-9 * chi0
+    assert _amax(T[:-1] - T0) <= 1e-9 and _amax(P - P0) <= 1e-9 * _amax(P0)
+    np.testing.assert_array_equal(T[-1], g.kf_Tcw[-1])
+    np.testing.assert_array_equal(ref["kf_Tcw"][-1], g.kf_Tcw[-1])
+
+
+def test_column_lane_large_nf_lds(solver):
+    """Two-sided column-lane factorisation with an x_p staging area past 64 KB of LDS (nf > 432 at
+    bw 9): the kernel's dynamic-LDS attribute must be raised for it."""
+    g = synth.generate("C1", n_kf=520, n_pt=9000, seed=909, track_min=2, track_max=10, fixed_frac=0.1)
+    out, ref = _run(solver, g)
+    st = solver.structure_stats()
+    assert st["bw"] == 9 and st["nf"] > 432, st
+    _check(out, ref)

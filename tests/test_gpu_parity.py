@@ -31,14 +31,22 @@ def test_lba_matches_oracle(solver, cfg):
     assert m["pt_level_diff"] == 0 and m["ln_level_diff"] == 0, m
     assert m["Tcw"] < EST_RTOL and m["pt"] < EST_RTOL and m["ln"] < EST_RTOL, m
     assert max(m["chi2_stage"]) < 1e-6, m
-    assert out["iters"][0] == ref["iters"][0]
-    # per-iteration χ² at linearisation agrees while the problem is not yet converged
+    # both optimize() calls run the same number of outer iterations
+    np.testing.assert_array_equal(out["iters"], ref["iters"])
+    # per-iteration trace of BOTH stages: same stage / iteration / trial count / result, χ² at
+    # linearisation and after the trial loop within 1e-6 (stage 2 is parity-unpinned against the
+    # reference itself: the oracle is a restatement, see oracle/refcpu.h)
     tg, tr = out["trace"], ref["trace"]
-    n = min(len(tg), len(tr))
-    for i in range(n):
-        if tr[i]["stage"] != tg[i]["stage"]:
-            break
-        assert abs(tg[i]["chi2_start"] - tr[i]["chi2_start"]) <= 1e-6 * abs(tr[i]["chi2_start"]), (i, tg[i], tr[i])
+    assert len(tg) == len(tr) == int(sum(max(i, 0) for i in ref["iters"])), (len(tg), len(tr))
+    for i in range(len(tr)):
+        for k in ("stage", "iter"):
+            assert tg[i][k] == tr[i][k], (i, k, tg[i], tr[i])
+        # damped-trial counts are decided by the sign of ρ; once an iteration's χ² decrease is at
+        # rounding level (converged) that sign is noise on either side, so compare them only before
+        if tr[i]["chi2_start"] - tr[i]["chi2_end"] > 1e-9 * tr[i]["chi2_start"]:
+            assert tg[i]["trials"] == tr[i]["trials"] and tg[i]["result"] == tr[i]["result"], (i, tg[i], tr[i])
+        for k in ("chi2_start", "chi2_end"):
+            assert abs(tg[i][k] - tr[i][k]) <= 1e-6 * abs(tr[i][k]), (i, k, tg[i], tr[i])
 
 
 def test_rerun_is_bitwise_deterministic(solver):

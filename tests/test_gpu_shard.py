@@ -39,6 +39,24 @@ def test_two_ranks_host_transport_match_oracle(tmp_path, cfg):
     _check(r[0], oa.lba_plucker(g))
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+def test_four_ranks_host_transport_match_oracle(tmp_path, cfg):
+    """configs[3]'s 4-way landmark sharding, the 4 ranks sharing the box's GPU (host transport)."""
+    import torch.multiprocessing as mp
+    world = 4
+    mp.spawn(dw.sharded_gpu_worker, args=(world, dw.free_port(), str(tmp_path), cfg, "host"), nprocs=world,
+             join=True)
+    r = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(world)]
+    g = synth.generate(cfg)
+    loc = [int(x["local_landmarks"]) for x in r]
+    assert all(0 < n < g.n_pt + g.n_ln for n in loc) and sum(loc) == g.n_pt + g.n_ln, loc
+    for i in range(1, world):
+        for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2", "ept_level", "iters", "trace_chi2"):
+            assert np.array_equal(r[0][k], r[i][k]), (i, k)
+    assert all(bool(x["rerun_equal"]) for x in r)
+    _check(r[0], oa.lba_plucker(g))
+
+
 def test_one_rank_rccl_transport_matches_oracle():
     from plba.lib import Solver, comm_unique_id
     g = synth.generate("C1L")
