@@ -238,12 +238,41 @@ const void *cl_kernel_impl(int bw, bool twisted, std::integer_sequence<int, B...
     return k;
 }
 // column-lane factorisation (plba_band_cl.hpp) for bandwidths up to kClMaxBW
-inline bool use_cl(int bw) { return bw >= 1 && bw <= kClMaxBW && !env_flag("PLBA_NO_CL"); }
+inline bool use_cl(int bw) {
+    const char *f = getenv("PLBA_FACTOR");
+    if (f && std::string(f) == "band") return false;
+    return bw >= 1 && bw <= kClMaxBW && !env_flag("PLBA_NO_CL");
+}
 inline size_t cl_lds_bytes(int bw, int nf, bool twisted) {
     return sizeof(double) * (cl_lds_doubles(bw) + (twisted ? (size_t)nf * 6 : 0));
 }
+template <int... B>
+const void *bcr_kernel_impl(int bw, std::integer_sequence<int, B...>) {
+    const void *k = nullptr;
+    ((bw == B ? (k = (const void *)k_rcs_factor_bcr<B>, 0) : 0), ...);
+    return k;
+}
+inline const void *bcr_kernel(int bw) { return bcr_kernel_impl(bw, std::make_integer_sequence<int, kBcrMaxBW + 1>{}); }
+inline size_t bcr_lds_bytes(int bw) { return sizeof(double) * bcr_lds_doubles(bw); }
+// Factorisation mode of a banded window: PLBA_FACTOR=bcr|cl|band forces one (diagnostics / A-B
+// runs); by default block cyclic reduction once the window has enough super-rows for its
+// log-depth chain to beat the two-sided column-lane chain of (nf+bw)/2 pivot steps.
+inline bool want_bcr(int bw, int nf) {
+    if (bw < 1 || bw > kBcrMaxBW) return false;
+    const int N = (nf + bw - 1) / bw;
+    if (N < 2 || N > kBcrMaxRows || bcr_lds_bytes(bw) > 159 * 1024) return false;
+    const char *f = getenv("PLBA_FACTOR");
+    if (f && f[0]) return std::string(f) == "bcr";
+    // measured crossover (profiles/r02): the two-sided column-lane chain wins at C3 (N = 13:
+    // 76 vs 116 µs), BCR at C4 (N = 52: 157 vs 230 µs) and C5 (N = 129: 198 vs 539 µs)
+    return N >= 24;
+}
 inline void launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
+    if (d.bcr) {
+        (void)hipLaunchKernel(bcr_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrNT), args, bcr_lds_bytes(d.bw), s);
+        return;
+    }
     if (d.cl) {
         const void *k = cl_kernel_impl(d.bw, d.twisted != 0, std::make_integer_sequence<int, kClMaxBW + 1>{});
         (void)hipLaunchKernel(k, dim3(d.twisted ? 2 : 1), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
@@ -554,8 +583,11 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // two-sided factorisation when the chain is long enough to halve and the separator's dense
     // system fits next to the band window in LDS (PLBA_NO_TWIST=1 disables, diagnostics only)
     const char *no_twist = getenv("PLBA_NO_TWIST");
-    const bool cl = band_mode && use_cl(bw);
-    const bool twisted = band_mode && bw >= 1 && nf >= 2 * bw + 16 &&
+    const bool bcr = band_mode && want_bcr(bw, nf);
+    d.bcr = bcr ? 1 : 0;
+    d.bcr_N = bcr ? (nf + bw - 1) / bw : 0;
+    const bool cl = band_mode && !bcr && use_cl(bw);
+    const bool twisted = band_mode && !bcr && bw >= 1 && nf >= 2 * bw + 16 &&
                          (cl ? cl_lds_bytes(bw, nf, true) : twisted_lds_bytes(bw, nf)) <= 159 * 1024 &&
                          !(no_twist && no_twist[0] == '1');
     d.cl = cl && cl_lds_bytes(bw, nf, twisted) <= 159 * 1024 ? 1 : 0;
@@ -657,6 +689,17 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ALLOC(d.tw_fail, 2);
         ALLOC(d.tw_count, 1);
     }
+    if (bcr) {
+        ALLOC(d.bcr_pub, (size_t)d.bcr_N * bcr_pub_doubles(bw));
+        ALLOC(d.bcr_x, (size_t)d.bcr_N * bcr_xrec(bw));
+        std::vector<int32_t> h_kf(nf, 0);
+        for (int k = 0; k < n_kf; ++k)
+            if (kf_hidx[k] >= 0) h_kf[kf_hidx[k]] = k;
+        UPLOAD(d.h_kf, h_kf);
+        ALLOC(d.bcr_flag, 2 * (size_t)d.bcr_N);
+        ALLOC(d.bcr_ctl, 4);
+        ALLOC(d.bcr_stamps, (size_t)d.bcr_N * kBcrStamps);
+    }
     ALLOC(d.bs, n);
     ALLOC(d.xp, n);
     ALLOC(d.Wbuf, (size_t)std::max(n, 1) * kTile);
@@ -668,7 +711,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * kPP);
     ALLOC(d.part_lm, std::max(d.n_lms_blocks, 1));
     ALLOC(d.part_lms, d.n_lms_blocks);
-    ALLOC(d.part_ps, d.n_kf_blocks);
+    d.n_ps = std::max(d.n_kf_blocks, d.bcr_N);
+    ALLOC(d.part_ps, d.n_ps);
     ALLOC(d.ctrl, 1);
     ALLOC(d.trace, kTraceCap);
     ALLOC(ctx->d_depth, Ep);
@@ -691,6 +735,11 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 #undef UPLOAD
     if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)band_lds_bytes(bw, nf)));
+    if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate
+        PLBA_CHECK(hipFuncSetAttribute(bcr_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bcr_lds_bytes(bw)));
+        PLBA_CHECK(hipMemset(d.bcr_flag, 0, 2 * sizeof(uint32_t) * (size_t)d.bcr_N));
+        PLBA_CHECK(hipMemset(d.bcr_ctl, 0, 4 * sizeof(uint32_t)));
+    }
     if (d.cl) {  // the column-lane kernel's LDS grows with nf (x_p staging of the two-sided variant)
         const void *k = cl_kernel_impl(bw, twisted, std::make_integer_sequence<int, kClMaxBW + 1>{});
         PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, twisted)));
@@ -887,6 +936,10 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
         launched += batch;
         int rc = read_ctrl(ctx);
         if (rc) return rc;
+        if (ctx->h_ctrl->dev_error) {
+            ctx->set_error("a bounded in-kernel hand-off wait timed out (workgroups not co-resident?)");
+            return PLBA_E_DEVICE;
+        }
         if (ctx->h_ctrl->all_done) break;
         if (launched >= max_steps) {
             ctx->set_error("LM schedule did not terminate after %d steps", launched);
@@ -1268,13 +1321,24 @@ int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [17][8] */) {
 #endif
 }
 
+// Diagnostics only (PLBA_DIAG bit 8): per-workgroup phase timestamps of the last block-cyclic-
+// reduction launch, [bcr_rows][32] s_memrealtime ticks (100 MHz).
+int plba_debug_bcr_stamps(plba_ctx *ctx, unsigned long long *out, int32_t cap, int32_t *rows) {
+    if (!ctx || !out || !rows) return PLBA_E_INVALID;
+    if (!ctx->uploaded || !ctx->d.bcr) return PLBA_E_STATE;
+    const int n = std::min(cap / kBcrStamps, ctx->d.bcr_N);
+    *rows = ctx->d.bcr_N;
+    PLBA_CHECK(hipMemcpy(out, ctx->d.bcr_stamps, sizeof(unsigned long long) * (size_t)n * kBcrStamps, hipMemcpyDeviceToHost));
+    return PLBA_OK;
+}
+
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[14] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+    const int64_t v[15] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
-                           ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl};
-    for (int i = 0; i < cap && i < 14; ++i) out[i] = v[i];
+                           ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N};
+    for (int i = 0; i < cap && i < 15; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

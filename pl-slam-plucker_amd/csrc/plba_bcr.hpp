@@ -1,0 +1,533 @@
+// Block cyclic reduction (BCR) of the banded reduced camera system, many workgroups.
+//
+// The column-lane factorisation (plba_band_cl.hpp) is a chain of nf/2 dependent 6x6 pivot
+// steps on two workgroups; at C4/C5 that chain is 184/454 steps. Here the band (bandwidth bw
+// pose blocks) is grouped into N = ceil(nf/bw) super-rows of S = 6·bw scalars, which makes it
+// block TRIDIAGONAL (super-row m couples only to m-1 and m+1). Cyclic reduction then eliminates
+// the odd super-rows, then every second remaining one, ... : level l eliminates the rows with
+// ctz(m) == l, each against its two neighbours a = m - 2^l and c = m + 2^l, and super-row 0 is
+// the root solved last. The chain is ceil(log2 N) + 1 dense eliminations instead of nf/2 6x6
+// pivot steps; every elimination of a level runs concurrently on its own workgroup.
+//
+// Eliminating row m (one workgroup, 512 threads, everything in LDS / registers):
+//   block LDLᵀ of D_m with 6x6 pivots, RHS = [U | V | b] = [A(m,a) | A(m,c) | b_m] carried along
+//   (right-looking, one 6x6 register tile per thread), and the Gram matrix
+//   G = RHSᵀ D_m⁻¹ RHS = Σ_k R'_kᵀ P_k⁻¹ R'_k accumulated in the same loop. Published:
+//     D_a -= G_UU, b_a -= G_Ub;  D_c -= G_VV, b_c -= G_Vb;  A(c,a) = F = -G_VU (new coupling).
+//   Then, off the critical path, X = D_m⁻¹ RHS (block back substitution), and once x_a and x_c
+//   are known: x_m = X_b - X_U x_a - X_V x_c.
+// The survivors pick up their neighbours' contributions level by level (fixed order: above,
+// then below, level by level — results do not depend on timing).
+//
+// Hand-offs (MI355X_MICROARCH.md, "Valid forms" table row 1): payload stored write-through
+// (sc1, __hip_atomic_store relaxed/agent), every storing wave drains vmcnt, workgroup barrier,
+// ONE lane stores the flag (relaxed agent atomic); the consumer polls the flag from one lane,
+// barrier, then every load of the payload is an sc1 load (__hip_atomic_load relaxed/agent).
+// Flags carry an epoch (launch count + 1) kept in bcr_ctl[0], advanced by the last workgroup
+// to finish (arrival counter), so nothing has to be cleared between launches or graph replays.
+// Every spin is bounded; a timeout raises Ctrl::dev_error (reported as PLBA_E_DEVICE).
+//
+// Reference semantics: LinearSolverEigen = SimplicialLDLT fails iff a pivot
+// is exactly 0. Every 6x6 pivot block is factorised LDLᵀ without pivoting, so its scalar pivots
+// are LDLᵀ pivots of the (reordered) system and a zero one fails the solve; x_p then keeps its
+// previous value (g2o still calls update()).
+//
+// Requires all N workgroups to be co-resident (one per CU, N <= kBcrMaxRows).
+
+constexpr int kBcrNT = 512;
+constexpr int kBcrMaxBW = 9;
+constexpr int kBcrMaxRows = 240;   // co-residency margin below the 256 CUs
+constexpr int kBcrParts = 12;      // partial sums per row of the x_m mat-vec
+
+__host__ __device__ constexpr int bcr_tri(int bw) { return bw * (bw + 1) / 2; }
+// Gram tiles: lower triangle of (2bw+1)x(2bw+1) 6x6 blocks over [U | V | b], minus the (b,b) corner
+__host__ __device__ constexpr int bcr_ngram(int bw) { return (2 * bw + 1) * (2 * bw + 2) / 2 - 1; }
+// LDS: D_m [S][S] | RHS [S][RS] (RS = 6(2bw+1): U, V, b padded to 6 columns) | W [S][S+RS] |
+//      x_a, x_c, x_m [3][S] | pivot factors [2][48] | mat-vec partials [kBcrParts][S] | poses [bw][24] + λ
+__host__ __device__ constexpr size_t bcr_lds_doubles(int bw) {
+    return (size_t)(6 * bw) * (6 * bw) + (size_t)(6 * bw) * (6 * (2 * bw + 1)) +
+           (size_t)(6 * bw) * (6 * bw + 6 * (2 * bw + 1)) + 3 * (size_t)(6 * bw) + 96 + (size_t)kBcrParts * (6 * bw) +
+           (size_t)bw * 24 + 2;
+}
+// published record of an eliminated super-row, element-major for coalesced write-through
+// stores: [36][ngram] Gram tiles (F = A(c,a) tiles stored negated) + 1 failure word
+__host__ __device__ constexpr size_t bcr_pub_doubles(int bw) { return (size_t)36 * bcr_ngram(bw) + 2; }
+// solution record of a super-row: x (6 bw) + failure word (propagated down the back substitution)
+__host__ __device__ constexpr int bcr_xrec(int bw) { return 6 * bw + 2; }
+
+__device__ __forceinline__ double ld_sc1(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one lane: relaxed poll until the flag carries `epoch`; bounded (~0.3 s), timeout -> *err = 1
+__device__ __forceinline__ bool bcr_poll(uint32_t *flag, uint32_t epoch, int32_t *err) {
+    for (uint32_t spins = 0;; ++spins) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return true;
+        if (spins >= (1u << 23)) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+// every storing wave drains its sc1 stores, then one lane raises the flag
+__device__ __forceinline__ void bcr_publish(uint32_t *flag, uint32_t epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void tri_decode(int t, int &i, int &j) {
+    i = 0;
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    j = t - i * (i + 1) / 2;
+}
+// 6x6 tile from LDS (row-major, leading dimension ld, 16-B aligned rows)
+__device__ __forceinline__ void lds_tile(const double *p, int ld, double (&t)[36]) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        const double2 *q = reinterpret_cast<const double2 *>(p + (size_t)r * ld);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double2 v = q[c];
+            t[r * 6 + 2 * c] = v.x;
+            t[r * 6 + 2 * c + 1] = v.y;
+        }
+    }
+}
+__device__ __forceinline__ void lds_tile_store(double *p, int ld, const double (&t)[36]) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        double2 *q = reinterpret_cast<double2 *>(p + (size_t)r * ld);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) q[c] = make_double2(t[r * 6 + 2 * c], t[r * 6 + 2 * c + 1]);
+    }
+}
+// LDLᵀ of a symmetric 6x6 block (lower triangle of p used): unit-lower l, 1/d; fail iff a pivot is 0
+__device__ __forceinline__ void ldl6(const double (&p)[36], double (&l)[36], double (&dinv)[6], bool &fail) {
+    double dd[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double w[6];
+#pragma unroll
+        for (int q = 0; q < j; ++q) w[q] = l[j * 6 + q] * dd[q];
+        double s = p[j * 6 + j];
+#pragma unroll
+        for (int q = 0; q < j; ++q) s = fma(-l[j * 6 + q], w[q], s);
+        dd[j] = s;
+        if (s == 0.0) fail = true;
+        dinv[j] = rcp_nr(s);
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            double t = p[i * 6 + j];
+#pragma unroll
+            for (int q = 0; q < j; ++q) t = fma(-l[i * 6 + q], w[q], t);
+            l[i * 6 + j] = t * dinv[j];
+        }
+    }
+}
+// v <- P⁻¹ v with P = L D Lᵀ
+__device__ __forceinline__ void ldl6_solve(const double (&l)[36], const double (&dinv)[6], double (&v)[6]) {
+#pragma unroll
+    for (int i = 1; i < 6; ++i)
+#pragma unroll
+        for (int q = 0; q < i; ++q) v[i] = fma(-l[i * 6 + q], v[q], v[i]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] *= dinv[i];
+#pragma unroll
+    for (int i = 4; i >= 0; --i)
+#pragma unroll
+        for (int q = i + 1; q < 6; ++q) v[i] = fma(-l[q * 6 + i], v[q], v[i]);
+}
+
+// PLBA_DIAG bit 8 (diagnostics only): per-workgroup phase timestamps (s_memrealtime, 100 MHz)
+// into bcr_stamps[m][kBcrStamps]; read with plba_debug_bcr_stamps / tools/bcr_stamps.py
+constexpr int kBcrStamps = 32;
+#define BCR_STAMP(slot)                                                                          \
+    do {                                                                                         \
+        if ((d.diag & 8) && threadIdx.x == 0)                                                    \
+            d.bcr_stamps[(size_t)blockIdx.x * kBcrStamps + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+// tile index of Gram block (u, v), u >= v
+__device__ __forceinline__ int gtile(int u, int v) { return u * (u + 1) / 2 + v; }
+
+template <int BW>
+__global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
+    TRIAL_GUARD
+    if constexpr (BW >= 1 && BW <= kBcrMaxBW) {
+        constexpr int NT = kBcrNT, S = 6 * BW, NB = 2 * BW + 1, RS = 6 * NB, WS = S + RS;
+        constexpr int TRI = bcr_tri(BW), NRT = BW * NB, NG = bcr_ngram(BW), XR = bcr_xrec(BW);
+        constexpr size_t PUB = bcr_pub_doubles(BW);
+        static_assert(TRI + NRT + NG <= NT, "one tile per thread");
+        static_assert(S + RS <= NT, "one W column per thread");
+        constexpr int NPART = NT / S < kBcrParts ? NT / S : kBcrParts;  // mat-vec slices per row
+        extern __shared__ __attribute__((aligned(16))) double lds[];
+        double *Dm = lds, *Rm = Dm + S * S, *Wm = Rm + S * RS, *xv = Wm + S * WS;  // xv: x_a | x_c | x_m
+        double *pv = xv + 3 * S;          // [2][48] pivot block factors: unit-lower L (36) + 1/d (6)
+        double *red = pv + 96;            // [kBcrParts][S]
+        double *ps = red + kBcrParts * S;  // [BW][24] Tcw | b_p | previous x_p of this row's poses, λ
+        __shared__ uint32_t s_epoch;
+        __shared__ int s_fail, s_last;
+        __shared__ double s_sum[NT / 64];
+        __shared__ int s_kf[BW + 1];
+        const int tid = threadIdx.x, m = blockIdx.x, N = d.bcr_N, nf = d.nf;
+        int L = 0;
+        while ((1 << L) < N) ++L;
+        const bool root = m == 0;
+        const int lm = root ? L : __builtin_ctz(m);
+        const int a_row = root ? -1 : m - (1 << lm), c_row = root ? N : m + (1 << lm);
+        const bool hasU = !root, hasC = !root && c_row < N;
+        BCR_STAMP(0);
+        if (tid == 0) {
+            s_epoch = __hip_atomic_load(&d.bcr_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+            s_fail = 0;
+        }
+        // ---- D_m (lower blocks; diagonal blocks full), b_m and, for odd m, the band couplings
+        //      U = A(m, m-1), V = A(m, m+1); rows past nf are identity / zero. Every global load of
+        //      a thread is issued before its LDS stores.
+        const size_t bstr = (size_t)(BW + 1) * 36;
+        const bool odd = (m & 1) != 0;
+        {
+            constexpr int ND = (S * S + NT - 1) / NT, NR = (S * RS + NT - 1) / NT;
+            double vd[ND], vr[NR];
+#pragma unroll
+            for (int u = 0; u < ND; ++u) {
+                const int t = tid + u * NT, r = t / S, c = t % S, bi = r / 6, bj = c / 6, i = m * BW + bi;
+                const bool ok = t < S * S && bi >= bj && i < nf;
+                // unconditional load from a clamped (always in-bounds) address, then select
+                const double g = d.Bd[ok ? (size_t)i * bstr + (bi - bj) * 36 + (r % 6) * 6 + c % 6 : 0];
+                vd[u] = ok ? g : (i >= nf && r == c ? 1.0 : 0.0);
+            }
+#pragma unroll
+            for (int u = 0; u < NR; ++u) {
+                const int t = tid + u * NT, r = t / RS, c = t % RS, bi = r / 6, bc = c / 6, ra = r % 6, cb = c % 6;
+                const int i = m * BW + bi, bj = bc - BW, j = (m + 1) * BW + bj;
+                size_t addr = 0;
+                int src = 0;  // 1: Bd, 2: bs
+                if (t < S * RS && i < nf) {
+                    if (bc < BW) {
+                        if (odd && bi <= bc) { src = 1; addr = (size_t)i * bstr + (BW + bi - bc) * 36 + ra * 6 + cb; }
+                    } else if (bc < 2 * BW) {
+                        if (odd && bj <= bi && j < nf) { src = 1; addr = (size_t)j * bstr + (BW + bj - bi) * 36 + cb * 6 + ra; }
+                    } else if (cb == 0) {
+                        src = 2;
+                        addr = (size_t)i * 6 + ra;
+                    }
+                }
+                const double g1 = d.Bd[src == 1 ? addr : 0], g2 = d.bs[src == 2 ? addr : 0];
+                vr[u] = src == 1 ? g1 : (src == 2 ? g2 : 0.0);
+            }
+#pragma unroll
+            for (int u = 0; u < ND; ++u)
+                if (tid + u * NT < S * S) Dm[tid + u * NT] = vd[u];
+#pragma unroll
+            for (int u = 0; u < NR; ++u)
+                if (tid + u * NT < S * RS) Rm[tid + u * NT] = vr[u];
+        }
+        for (int t = tid; t < S * WS; t += NT) Wm[t] = 0.0;
+        // this super-row's poses (updated at the very end): current Tcw, b_p, previous x_p, λ
+        // staged now, off the critical path; fixed poses k ≡ m (mod N) copied to the trial state
+        const int cur0 = d.ctrl->cur;
+        {
+            const double *Tc0 = d.Tb[cur0];
+            double *Tt0 = d.Tb[cur0 ^ 1];
+            if (tid < BW) s_kf[tid] = m * BW + tid < nf ? d.h_kf[m * BW + tid] : 0;
+            for (int t = tid; t < BW * 24; t += NT) {
+                const int i = t / 24, q = t % 24, h = m * BW + i;
+                double v = 0.0;
+                if (h < nf) {
+                    const int kf = d.h_kf[h];
+                    v = q < 12 ? Tc0[(size_t)kf * 12 + q] : (q < 18 ? d.bp[(size_t)h * 6 + q - 12] : d.xp[(size_t)h * 6 + q - 18]);
+                }
+                ps[t] = v;
+            }
+            if (tid == 0) ps[BW * 24] = d.ctrl->lambda;
+            for (int k = m + N * tid; k < d.n_kf; k += N * NT)
+                if (d.kf_hidx[k] < 0)
+#pragma unroll
+                    for (int q = 0; q < 12; ++q) Tt0[(size_t)k * 12 + q] = Tc0[(size_t)k * 12 + q];
+        }
+        __syncthreads();
+        BCR_STAMP(1);
+        // ---- survivor phases: contributions of the neighbours eliminated at levels < lm. Every
+        //      sc1 load of a phase is issued before the first use (no per-element round trip).
+        double fail_in = 0.0;  // failure words flowing in (forward)
+        for (int lp = 0; lp < lm; ++lp) {
+            const int na = m - (1 << lp), nb = m + (1 << lp);  // above (m is its c) / below (m is its a)
+            const bool ha = na >= 0, hb = nb < N;
+            if (tid == 0 && ha && !bcr_poll(&d.bcr_flag[2 * na], s_epoch, &d.ctrl->dev_error)) s_fail = 1;
+            if (tid == 64 && hb && !bcr_poll(&d.bcr_flag[2 * nb], s_epoch, &d.ctrl->dev_error)) s_fail = 1;
+            __syncthreads();
+            const double *pa = d.bcr_pub + (size_t)(ha ? na : 0) * PUB, *pb = d.bcr_pub + (size_t)(hb ? nb : 0) * PUB;
+            const bool takeF = lm == lp + 1;  // the coupling created at level lm-1: U from above, V from below
+            const bool fU = takeF && ha && !root, fV = takeF && hb && hasC;
+            constexpr int KD = (TRI * 36 + NT - 1) / NT, KF = (S * S + NT - 1) / NT;
+            double gda[KD], gdb[KD], gfa[KF], gfb[KF], gba = 0.0, gbb = 0.0, fa = 0.0, fb = 0.0;
+            // D_m -= G_VV(above) + G_UU(below)   (lower blocks, element-major records)
+#pragma unroll
+            for (int u = 0; u < KD; ++u) {
+                const int t = tid + u * NT, blk = t % TRI, e = t / TRI;
+                int bi, bj;
+                tri_decode(blk, bi, bj);
+                const bool ok = t < TRI * 36;
+                gda[u] = ok && ha ? ld_sc1(pa + (size_t)e * NG + gtile(BW + bi, BW + bj)) : 0.0;
+                gdb[u] = ok && hb ? ld_sc1(pb + (size_t)e * NG + gtile(bi, bj)) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < KF; ++u) {
+                const int t = tid + u * NT, blk = t % (BW * BW), e = t / (BW * BW), vb = blk / BW, ub = blk % BW;
+                const bool ok = t < S * S;
+                const size_t o = (size_t)e * NG + gtile(BW + vb, ub);  // F = A(c_n, a_n) (stored negated)
+                gfa[u] = ok && fU ? ld_sc1(pa + o) : 0.0;
+                gfb[u] = ok && fV ? ld_sc1(pb + o) : 0.0;
+            }
+            if (tid < S) {  // b_m -= g_Vb(above) + g_Ub(below): row 0 of the b-row tiles
+                const int vb = tid / 6, e = tid % 6;
+                gba = ha ? ld_sc1(pa + (size_t)e * NG + gtile(2 * BW, BW + vb)) : 0.0;
+                gbb = hb ? ld_sc1(pb + (size_t)e * NG + gtile(2 * BW, vb)) : 0.0;
+            }
+            if (tid == 0) {
+                fa = ha ? ld_sc1(pa + (size_t)36 * NG) : 0.0;
+                fb = hb ? ld_sc1(pb + (size_t)36 * NG) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < KD; ++u) {
+                const int t = tid + u * NT, blk = t % TRI, e = t / TRI;
+                if (t < TRI * 36) {
+                    int bi, bj;
+                    tri_decode(blk, bi, bj);
+                    Dm[(6 * bi + e / 6) * S + 6 * bj + e % 6] -= gda[u] + gdb[u];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < KF; ++u) {
+                const int t = tid + u * NT, blk = t % (BW * BW), e = t / (BW * BW), vb = blk / BW, ub = blk % BW;
+                const int ea = e / 6, eb = e % 6;
+                if (t < S * S) {
+                    if (fU) Rm[(6 * vb + ea) * RS + 6 * ub + eb] = gfa[u];       // U_m = A(m, a_n), m = c_n
+                    if (fV) Rm[(6 * ub + eb) * RS + S + 6 * vb + ea] = gfb[u];   // V_m = A(c_n, m)ᵀ
+                }
+            }
+            if (tid < S) Rm[tid * RS + 2 * S] -= gba + gbb;
+            if (tid == 0) fail_in += fa + fb;
+            __syncthreads();
+            BCR_STAMP(2 + lp);
+        }
+        // ---- elimination of super-row m. One 6x6 tile per thread, kept in registers:
+        //      D tiles (i >= j), RHS tiles (i, column block), Gram tiles (u >= v); every tile does
+        //      acc += A·B per step with A = -D(i,k) (D, RHS) or R'(k,u)ᵀ (Gram), B = W(k, ·).
+        auto rhs_on = [&](int bc) { return bc == 2 * BW || (bc < BW ? hasU : hasC); };
+        int role = 0, ti = 0, tj = 0;
+        if (tid < TRI) {
+            role = 1;
+            tri_decode(tid, ti, tj);
+        } else if (tid < TRI + NRT) {
+            role = 2;
+            ti = (tid - TRI) / NB;
+            tj = (tid - TRI) % NB;
+            if (!rhs_on(tj)) role = 0;
+        } else if (tid < TRI + NRT + NG) {
+            role = 3;
+            tri_decode(tid - TRI - NRT, ti, tj);
+            if (root || !rhs_on(ti) || !rhs_on(tj)) role = 0;
+        }
+        double acc[36];
+        if (role == 1) lds_tile(Dm + (6 * ti) * S + 6 * tj, S, acc);
+        else if (role == 2) lds_tile(Rm + (6 * ti) * RS + 6 * tj, RS, acc);
+        else {
+#pragma unroll
+            for (int e = 0; e < 36; ++e) acc[e] = 0.0;
+        }
+        bool fail = false;
+        auto factor_pivot = [&](const double (&p)[36], double *dst) {
+            double l[36], dinv[6];
+#pragma unroll
+            for (int e = 0; e < 36; ++e) l[e] = 0.0;
+            ldl6(p, l, dinv, fail);
+#pragma unroll
+            for (int e = 0; e < 36; ++e) dst[e] = l[e];
+#pragma unroll
+            for (int e = 0; e < 6; ++e) dst[36 + e] = dinv[e];
+        };
+        if (tid == 0) factor_pivot(acc, pv);  // tile (0,0) = P_0
+        __syncthreads();
+        const int nU = hasU ? S : 0, nV = hasC ? S : 0;
+        for (int k = 0; k < BW; ++k) {
+            const double *pk = pv + 48 * (k & 1);
+            // phase 1: W(k, col) = P_k⁻¹ M(k, col) for the D columns of later blocks and the
+            // active RHS columns (P_k factors broadcast from LDS)
+            const int nWd = S - 6 * (k + 1);
+            if (tid < nWd + nU + nV + 1 && !(d.diag & 32)) {  // (diag 32/16: timing experiments only)
+                double v[6];
+                int col;
+                if (tid < nWd) {
+                    const int j = 6 * (k + 1) + tid;  // M(k, j) = D(j, k)ᵀ (lower storage)
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) v[q] = Dm[j * S + 6 * k + q];
+                    col = j;
+                } else {
+                    int cc = tid - nWd;
+                    cc = cc < nU ? cc : (cc - nU < nV ? S + (cc - nU) : 2 * S);
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) v[q] = Rm[(6 * k + q) * RS + cc];
+                    col = S + cc;
+                }
+                double l[36], dinv[6];
+#pragma unroll
+                for (int e = 0; e < 36; ++e) l[e] = pk[e];
+#pragma unroll
+                for (int e = 0; e < 6; ++e) dinv[e] = pk[36 + e];
+                ldl6_solve(l, dinv, v);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) Wm[(6 * k + q) * WS + col] = v[q];
+            }
+            __syncthreads();
+            // phase 2
+            const bool act = (role == 1 && tj > k) || (role == 2 && ti > k) || role == 3;
+            if (act && !(d.diag & 16)) {
+                double at[36], bt[36];
+                if (role == 3) {
+                    double rt[36];
+                    lds_tile(Rm + (6 * k) * RS + 6 * ti, RS, rt);
+#pragma unroll
+                    for (int q = 0; q < 6; ++q)
+#pragma unroll
+                        for (int ea = 0; ea < 6; ++ea) at[ea * 6 + q] = rt[q * 6 + ea];
+                } else {
+                    lds_tile(Dm + (6 * ti) * S + 6 * k, S, at);
+#pragma unroll
+                    for (int e = 0; e < 36; ++e) at[e] = -at[e];
+                }
+                const int wc = role == 1 ? 6 * tj : S + 6 * tj;
+                lds_tile(Wm + (6 * k) * WS + wc, WS, bt);
+#pragma unroll
+                for (int ea = 0; ea < 6; ++ea)
+#pragma unroll
+                    for (int q = 0; q < 6; ++q)
+#pragma unroll
+                        for (int eb = 0; eb < 6; ++eb) acc[ea * 6 + eb] = fma(at[ea * 6 + q], bt[q * 6 + eb], acc[ea * 6 + eb]);
+                if (role == 1 && tj == k + 1) {
+                    lds_tile_store(Dm + (6 * ti) * S + 6 * tj, S, acc);
+                    if (ti == k + 1) factor_pivot(acc, pv + 48 * ((k + 1) & 1));  // next pivot block
+                }
+                if (role == 2 && ti == k + 1) lds_tile_store(Rm + (6 * ti) * RS + 6 * tj, RS, acc);
+            }
+            __syncthreads();
+            BCR_STAMP(20 + k);
+        }
+        if (fail) s_fail = 1;  // (benign race: every writer stores 1)
+        BCR_STAMP(12);
+        const uint32_t epoch = s_epoch;
+        __syncthreads();
+        const double fail_fwd = fail_in + (s_fail ? 1.0 : 0.0);  // meaningful on tid 0
+        // ---- publish the Gram tiles (element-major, coalesced write-through) + failure word
+        if (!root) {
+            double *pub = d.bcr_pub + (size_t)m * PUB;
+            if (role == 3) {
+                const int gt = tid - TRI - NRT;
+                const double sg = (ti >= BW && ti < 2 * BW && tj < BW) ? -1.0 : 1.0;  // F = -G_VU
+#pragma unroll
+                for (int e = 0; e < 36; ++e) st_sc1(pub + (size_t)e * NG + gt, sg * acc[e]);
+            }
+            if (tid == 0) st_sc1(pub + (size_t)36 * NG, fail_fwd);
+            bcr_publish(&d.bcr_flag[2 * m], epoch);
+        }
+        BCR_STAMP(13);
+        // ---- X = D_m⁻¹ RHS (block back substitution, right-looking, into Rm) for the active
+        //      columns; x_m = X_b - X_U x_a - X_V x_c once the neighbours are solved
+        const int ncol = nU + nV + 1;
+        for (int t = tid; t < S * ncol; t += NT) {
+            const int r = t / ncol, cc0 = t % ncol;
+            const int cc = cc0 < nU ? cc0 : (cc0 - nU < nV ? S + (cc0 - nU) : 2 * S);
+            Rm[r * RS + cc] = Wm[r * WS + S + cc];
+        }
+        __syncthreads();
+        for (int j = BW - 1; j >= 1; --j) {
+            for (int t = tid; t < 6 * j * ncol; t += NT) {
+                const int r = t / ncol, cc0 = t % ncol;
+                const int cc = cc0 < nU ? cc0 : (cc0 - nU < nV ? S + (cc0 - nU) : 2 * S);
+                double sacc = Rm[r * RS + cc];
+#pragma unroll
+                for (int p = 0; p < 6; ++p) sacc = fma(-Wm[r * WS + 6 * j + p], Rm[(6 * j + p) * RS + cc], sacc);
+                Rm[r * RS + cc] = sacc;
+            }
+            __syncthreads();
+        }
+        BCR_STAMP(14);
+        double *xa = xv, *xc = xv + S, *xm = xv + 2 * S;
+        double fail_tot = fail_fwd;  // root: everything has flowed in; others: from a (and c)
+        if (!root) {
+            if (tid == 0 && !bcr_poll(&d.bcr_flag[2 * a_row + 1], epoch, &d.ctrl->dev_error)) s_fail = 1;
+            if (hasC && tid == 64 && !bcr_poll(&d.bcr_flag[2 * c_row + 1], epoch, &d.ctrl->dev_error)) s_fail = 1;
+            __syncthreads();
+            for (int t = tid; t < S; t += NT) {
+                xa[t] = ld_sc1(d.bcr_x + (size_t)a_row * XR + t);
+                xc[t] = hasC ? ld_sc1(d.bcr_x + (size_t)c_row * XR + t) : 0.0;
+            }
+            if (tid == 0) fail_tot = ld_sc1(d.bcr_x + (size_t)a_row * XR + S) + (s_fail ? 1.0 : 0.0);
+            __syncthreads();
+            BCR_STAMP(15);
+            // mat-vec in kBcrParts column slices per row, partials summed in slice order
+            if (tid < S * NPART) {
+                const int r = tid % S, part = tid / S;
+                constexpr int CPP = (2 * S + NPART - 1) / NPART;
+                double sacc = 0.0;
+#pragma unroll
+                for (int u = 0; u < CPP; ++u) {
+                    const int q = part * CPP + u;
+                    if (q < S) sacc = fma(Rm[r * RS + q], xa[q], sacc);
+                    else if (q < 2 * S && hasC) sacc = fma(Rm[r * RS + q], xc[q - S], sacc);
+                }
+                red[part * S + r] = sacc;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) s_fail = fail_tot != 0.0 ? 1 : 0;
+        for (int r = tid; r < S; r += NT) {
+            double sacc = Rm[r * RS + 2 * S];
+            if (!root)
+                for (int part = 0; part < NPART; ++part) sacc -= red[part * S + r];
+            xm[r] = sacc;
+            st_sc1(d.bcr_x + (size_t)m * XR + r, sacc);
+        }
+        if (tid == 0) {
+            st_sc1(d.bcr_x + (size_t)m * XR + S, fail_tot);
+            if (root) d.ctrl->solve_ok = fail_tot != 0.0 ? 0 : 1;
+        }
+        bcr_publish(&d.bcr_flag[2 * m + 1], epoch);
+        BCR_STAMP(16);
+        // ---- this super-row's poses: x_p (kept from the previous trial if the solve failed, A13),
+        //      oplus into the trial state, pose part of Σx(λx+b)
+        const bool failed = s_fail != 0;
+        const double lam = ps[BW * 24];
+        double sc = 0.0;
+        if (tid < BW) {
+            const int h = m * BW + tid;
+            if (h < nf) {
+                const double *pp = ps + tid * 24;
+                double x[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) x[q] = failed ? pp[18 + q] : xm[6 * tid + q];
+                if (!failed)
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) d.xp[6 * h + q] = x[q];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) sc += x[q] * (lam * x[q] + pp[12 + q]);
+                pose_oplus(pp, x, d.Tb[cur0 ^ 1] + (size_t)s_kf[tid] * 12);
+            }
+        }
+        const double ssum = block_sum<NT>(sc, s_sum);
+        if (tid == 0) d.part_ps[m] = ssum;
+        // ---- arrival: the last workgroup advances the epoch for the next launch
+        if (tid == 0) {
+            const uint32_t old = __hip_atomic_fetch_add(&d.bcr_ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == (uint32_t)(N - 1)) {
+                __hip_atomic_store(&d.bcr_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d.bcr_ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        BCR_STAMP(17);
+    }
+}

@@ -63,7 +63,8 @@ struct Ctrl {
     int32_t stage_robust[2], stage_level[2], stage_classify[2];
     int32_t max_trials, ntrace, any_active, cur;      // cur: which state buffer is current
     int32_t steps;                                     // step graphs that did work (diagnostic)
-    int32_t pad[3];
+    int32_t dev_error;                                 // a bounded in-kernel wait timed out
+    int32_t pad[2];
 };
 
 // All device pointers of one window (passed by value to every kernel).
@@ -119,7 +120,9 @@ struct Dev {
     int32_t *part_any;                  // [n_lm_blocks] block has an active landmark
     double *part_max;                   // [nf + n_lm_blocks] (landmark part from nf on)
     double *part_lm, *part_lms;         // [n_lms_blocks] trial χ² partials, scale partials (k_lm_solve)
-    double *part_ps;                    // [n_kf_blocks]
+    double *part_ps;                    // [n_ps] pose part of Σx(λx+b) (one slot per factorisation workgroup)
+    int32_t n_ps;                       // max(n_kf_blocks, bcr_N)
+    int32_t *h_kf;                      // [nf] keyframe of each free-pose Hessian index
     Ctrl *ctrl;
     plba_iter_trace *trace;             // [kTraceCap] per-iteration records written by k_decide
     // sharded windows: the arrays the ranks sum with one all-reduce each
@@ -143,6 +146,13 @@ struct Dev {
     double *Lband2, *Kinv2, *zb2;       // factors of the bottom segment (reversed numbering)
     double *tw_sep;                     // [2][bw][bw+1][36] + [2][bw][6] separator windows
     int32_t *tw_fail, *tw_count;        // [2] per-segment failure, arrival counter
+    // block cyclic reduction over super-rows of bw pose blocks (plba_bcr.hpp)
+    int32_t bcr, bcr_N;                 // enabled; super-rows (= workgroups of the launch)
+    double *bcr_pub;                    // [N][bcr_pub_doubles(bw)] Schur contributions + coupling
+    double *bcr_x;                      // [N][6 bw] solution of each super-row
+    uint32_t *bcr_flag;                 // [N][2] forward / backward hand-off flags (epoch)
+    uint32_t *bcr_ctl;                  // [4] epoch, arrival counter, failure, spare
+    unsigned long long *bcr_stamps;     // [N][32] phase timestamps (PLBA_DIAG bit 8 only)
 };
 
 
@@ -684,7 +694,7 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
         }
     }
     const double s = block_sum<NT>(sc, sh_pu);
-    for (int i = threadIdx.x; i < d.n_kf_blocks; i += NT) d.part_ps[i] = i == 0 ? s : 0.0;
+    for (int i = threadIdx.x; i < d.n_ps; i += NT) d.part_ps[i] = i == 0 ? s : 0.0;
 }
 
 // Envelope-aware tiled LDLᵀ of the lower triangle + solve, one workgroup of 1024 threads.
@@ -1458,6 +1468,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d) {
 }
 
 #include "plba_band_cl.hpp"
+#include "plba_bcr.hpp"
 
 // ---------------------------------------------------------------- update + trial evaluation
 // stand-alone pose update (windows without free poses: no factorisation kernel to fuse into)
@@ -1856,7 +1867,7 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
         for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) a += d.part_lm[i];
         for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) b += d.part_lms[i];
     }
-    for (int i = threadIdx.x; i < d.n_kf_blocks; i += kBlock) b += d.part_ps[i];  // poses: replicated
+    for (int i = threadIdx.x; i < d.n_ps; i += kBlock) b += d.part_ps[i];  // poses: replicated
     double tempChi0 = block_sum<kBlock>(a, sh);
     double scale0 = block_sum<kBlock>(b, sh);
     if (d.sharded) {  // landmark terms summed over ranks

@@ -297,3 +297,29 @@ def test_column_lane_large_nf_lds(solver):
     st = solver.structure_stats()
     assert st["bw"] == 9 and st["nf"] > 432, st
     _check(out, ref)
+
+
+@pytest.mark.parametrize("tmax,n_kf", [(2, 12), (3, 30), (5, 40), (8, 64), (8, 100), (10, 60), (10, 130)])
+def test_block_cyclic_reduction_matches_oracle(solver, monkeypatch, tmax, n_kf):
+    """Block cyclic reduction over super-rows of bw pose blocks (plba_bcr.hpp), forced on, at
+    bandwidths 1..9 and super-row counts 2..16 (odd and even, powers of two and not), against
+    the oracle and against the column-lane factorisation of the same window."""
+    g = synth.generate("C1L", n_kf=n_kf, n_pt=25 * n_kf, n_ln=5 * n_kf, seed=500 + tmax + n_kf,
+                       track_min=2, track_max=tmax, fixed_frac=0.1)
+    ref = oa.lba_plucker(g)
+    monkeypatch.setenv("PLBA_FACTOR", "bcr")
+    solver.upload(g)
+    st = solver.structure_stats()
+    assert st["banded"] == 1 and st["bcr_rows"] == -(-st["nf"] // st["bw"]) >= 2, st
+    out = solver.lba_plucker()
+    _check(out, ref)
+    solver.reset()
+    again = solver.lba_plucker()          # epoch-tagged hand-offs: a rerun is bitwise identical
+    for k in ("kf_Tcw", "pt_xyz", "ln_orth"):
+        assert np.array_equal(out[k], again[k]), k
+    monkeypatch.setenv("PLBA_FACTOR", "cl")
+    solver.upload(g)
+    assert solver.structure_stats()["bcr_rows"] == 0
+    cl = solver.lba_plucker()
+    monkeypatch.delenv("PLBA_FACTOR")
+    assert np.abs(out["kf_Tcw"] - cl["kf_Tcw"]).max() < 1e-9
