@@ -69,8 +69,18 @@ struct plba_ctx {
         double *hbuf = nullptr;  // pinned staging (HOST)
         size_t hcap = 0;
     } comm;
-    // device arena
-    std::vector<void *> allocs;
+    // device arena: ONE grow-only allocation carved per window (no hipMalloc / hipFree per
+    // upload), filled by one memset and one host->device copy from pinned staging
+    struct Item {
+        void **field;
+        size_t bytes, src_bytes;
+        const void *src;
+        bool zero;
+        size_t off;
+    };
+    std::vector<Item> plan;
+    char *arena = nullptr, *staging = nullptr;
+    size_t arena_cap = 0, staging_cap = 0;
     Ctrl *h_ctrl = nullptr;  // pinned
     uint8_t *d_depth = nullptr;  // [Ep] isDepthPositive flags
     // host-side bookkeeping
@@ -122,31 +132,75 @@ struct plba_ctx {
             multi_exec[i] = nullptr;
             multi_graph[i] = nullptr;
         }
-        for (void *p : allocs) (void)hipFree(p);
-        allocs.clear();
+        plan.clear();
         d = Dev{};
         uploaded = initialized = false;
     }
+    // Records a device array of `count` T (at least 128 bytes: kernels issue unconditional
+    // loads of one record for dead lanes, which must stay inside the array). `src` (host, kept
+    // alive until commit_plan) is uploaded; everything else starts zeroed (`zero`: must stay
+    // zero even under PLBA_POISON).
     template <typename T>
-    int alloc(T *&p, size_t count) {
+    void alloc(T *&p, size_t count, const void *src = nullptr, bool zero = false) {
         p = nullptr;
-        // at least 128 bytes, zero-filled when the array is (nearly) empty: kernels issue
-        // unconditional loads of one record (an edge's 12 A doubles, a pose's 6 x_p doubles)
-        // for dead lanes, which must stay inside the allocation and read defined indices
-        const bool tiny = count * sizeof(T) < 128;
-        if (tiny) count = (128 + sizeof(T) - 1) / sizeof(T);
-        hipError_t e = hipMalloc((void **)&p, count * sizeof(T));
-        if (e != hipSuccess) {
-            set_error("hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
-            return PLBA_E_NOMEM;
+        const size_t sb = count * sizeof(T);
+        plan.push_back(Item{(void **)&p, std::max(sb, (size_t)128), src ? sb : 0, src, zero, 0});
+    }
+    int commit_plan() {
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        size_t up = 0, tot = 0;
+        for (auto &it : plan)
+            if (it.src) { it.off = up; up = al(up + it.bytes); }
+        tot = up;
+        for (auto &it : plan)
+            if (!it.src) { it.off = tot; tot = al(tot + it.bytes); }
+        if (tot > arena_cap) {
+            (void)hipStreamSynchronize(stream);
+            if (arena) (void)hipFree(arena);
+            arena = nullptr;
+            arena_cap = 0;
+            const size_t cap = tot + tot / 4;
+            if (hipMalloc((void **)&arena, cap) != hipSuccess) {
+                (void)hipGetLastError();
+                set_error("hipMalloc(%zu bytes) of the window arena failed", cap);
+                return PLBA_E_NOMEM;
+            }
+            arena_cap = cap;
         }
-        allocs.push_back(p);
-        if (tiny) (void)hipMemset(p, 0, count * sizeof(T));
-        if constexpr (std::is_same<T, double>::value) {
-            // PLBA_POISON=1 (diagnostics only): fill f64 buffers with NaN to expose reads of
-            // memory no kernel wrote (a reused allocation is not zero).
-            const char *poison = getenv("PLBA_POISON");
-            if (poison && poison[0] == '1') (void)hipMemset(p, 0xFF, count * sizeof(T));
+        if (up > staging_cap) {
+            (void)hipStreamSynchronize(stream);
+            if (staging) (void)hipHostFree(staging);
+            staging = nullptr;
+            staging_cap = 0;
+            const size_t cap = up + up / 4;
+            if (hipHostMalloc((void **)&staging, cap, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                set_error("hipHostMalloc(%zu bytes) of the upload staging failed", cap);
+                return PLBA_E_NOMEM;
+            }
+            staging_cap = cap;
+        }
+        for (auto &it : plan) {
+            *it.field = arena + it.off;
+            if (it.src) {
+                if (it.src_bytes) std::memcpy(staging + it.off, it.src, it.src_bytes);
+                if (it.bytes > it.src_bytes) std::memset(staging + it.off + it.src_bytes, 0, it.bytes - it.src_bytes);
+            }
+        }
+        // PLBA_POISON=1 (diagnostics only): non-uploaded arrays start as NaN (0xFF bytes) to expose
+        // reads of memory no kernel wrote; arrays whose zero start is part of the contract stay 0
+        const char *poison = getenv("PLBA_POISON");
+        const bool pz = poison && poison[0] == '1';
+        hipError_t e = hipMemsetAsync(arena + up, pz ? 0xFF : 0, tot - up, stream);
+        if (e == hipSuccess && pz)
+            for (auto &it : plan)
+                if (it.zero && e == hipSuccess) e = hipMemsetAsync(arena + it.off, 0, it.bytes, stream);
+        if (e == hipSuccess && up) e = hipMemcpyAsync(arena, staging, up, hipMemcpyHostToDevice, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("window arena fill failed: %s", hipGetErrorString(e));
+            return PLBA_E_DEVICE;
         }
         return PLBA_OK;
     }
@@ -263,9 +317,14 @@ inline bool want_bcr(int bw, int nf) {
     if (N < 2 || N > kBcrMaxRows || bcr_lds_bytes(bw) > 159 * 1024) return false;
     const char *f = getenv("PLBA_FACTOR");
     if (f && f[0]) return std::string(f) == "bcr";
-    // measured crossover (profiles/r02): the two-sided column-lane chain wins at C3 (N = 13:
-    // 76 vs 116 µs), BCR at C4 (N = 52: 157 vs 230 µs) and C5 (N = 129: 198 vs 539 µs)
-    return N >= 24;
+    // latency model calibrated on C3/C4/C5 (profiles/r02): the two-sided column-lane
+    // chain costs ~1.3 µs per pivot block, (nf + bw)/2 of them; BCR ~(2.6·bw + 4.8) µs per level,
+    // ceil(log2 N) + 1 levels. C3 (N = 13): 76 vs 116 µs -> column lane; C4 (N = 52): 230 vs
+    // 157 µs and C5 (N = 129): 539 vs 198 µs -> BCR.
+    int levels = 1;
+    while ((1 << (levels - 1)) < N) ++levels;
+    const double t_cl = 1.3 * (nf + bw) / 2.0, t_bcr = levels * (2.6 * bw + 4.8);
+    return t_bcr < t_cl;
 }
 inline void launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
@@ -327,13 +386,6 @@ int collect_timing(plba_ctx *ctx) {
     return PLBA_OK;
 }
 
-template <typename T>
-int upload_vec(plba_ctx *ctx, T *&dst, const std::vector<T> &src) {
-    int rc = ctx->alloc(dst, src.size());
-    if (rc) return rc;
-    if (!src.empty()) PLBA_CHECK(hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
-    return PLBA_OK;
-}
 
 // ------------------------------------------------------------------ upload / structure prep
 int do_upload(plba_ctx *ctx, const plba_graph *g) {
@@ -358,7 +410,15 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             ctx->set_error("line edge %d references a missing vertex", e);
             return PLBA_E_INVALID;
         }
+    auto tmark = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        const auto t = std::chrono::steady_clock::now();
+        if (env_flag("PLBA_TIMING"))
+            fprintf(stderr, "[plba upload] %-24s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - tmark).count());
+        tmark = t;
+    };
     ctx->free_all();
+    mark("free");
     const int n_kf = g->n_kf, n_pt_g = g->n_pt, n_ln_g = g->n_ln, Ep_g = g->n_ept, El_g = g->n_eln;
     const int R = ctx->comm.nranks, rank = ctx->comm.rank;
     ctx->n_kf = n_kf; ctx->n_pt = n_pt_g; ctx->n_ln = n_ln_g; ctx->Ep = Ep_g; ctx->El = El_g;
@@ -380,16 +440,25 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         std::vector<int32_t> key_pt(n_pt_g, INT32_MAX), key_ln(n_ln_g, INT32_MAX);
         for (int e = Ep_g - 1; e >= 0; --e) key_pt[g->ept_lm[e]] = kpos[g->ept_kf[e]];
         for (int e = El_g - 1; e >= 0; --e) key_ln[g->eln_lm[e]] = kpos[g->eln_kf[e]];
-        std::vector<int32_t> ord;
-        for (int p = 0; p < n_pt_g; ++p)
-            if (pt_owner[p] == rank) ord.push_back(p);
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key_pt[a] < key_pt[b]; });
-        for (int p : ord) { pt_loc[p] = n_pt++; lm_gpos.push_back(p); }
-        ord.clear();
-        for (int l = 0; l < n_ln_g; ++l)
-            if (ln_owner[l] == rank) ord.push_back(l);
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key_ln[a] < key_ln[b]; });
-        for (int l : ord) { ln_loc[l] = n_ln++; lm_gpos.push_back(n_pt_g + l); }
+        // stable counting sort by key (key in [0, n_kf], n_kf = never observed)
+        auto order = [&](int n, const std::vector<int32_t> &own, const std::vector<int32_t> &key,
+                         std::vector<int32_t> &loc, int &cnt, int gbase) {
+            std::vector<int32_t> c(n_kf + 2, 0);
+            for (int i = 0; i < n; ++i)
+                if (own[i] == rank) c[std::min(key[i], n_kf) + 1]++;
+            for (int k = 0; k <= n_kf; ++k) c[k + 1] += c[k];
+            const int base = (int)lm_gpos.size();
+            lm_gpos.resize(base + c[n_kf + 1]);
+            for (int i = 0; i < n; ++i)
+                if (own[i] == rank) {
+                    const int pos = c[std::min(key[i], n_kf)]++;
+                    loc[i] = pos;
+                    lm_gpos[base + pos] = gbase + i;
+                }
+            cnt = (int)lm_gpos.size() - base;
+        };
+        order(n_pt_g, pt_owner, key_pt, pt_loc, n_pt, 0);
+        order(n_ln_g, ln_owner, key_ln, ln_loc, n_ln, n_pt_g);
     }
     ctx->lm_gpos = lm_gpos;
     int Ep = 0, El = 0;
@@ -444,6 +513,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ctx->e_orig = e_orig;
     ctx->h_level.assign(E, 0);
 
+    mark("landmark order + CSR");
     // free-pose-major edge lists (ascending CSR edge index)
     std::vector<int32_t> pe_off(nf + 1, 0);
     for (int e = 0; e < E; ++e)
@@ -456,88 +526,76 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             if (e_hidx[e] >= 0) pe_list[f[e_hidx[e]]++] = e;
     }
 
-    // reduced-camera block pattern + triples (e1 at pose i1 <= e2 at pose i2, same landmark).
-    // The pattern is that of the WHOLE window on every rank (the all-reduced value array must
-    // have one layout); triples come from the local landmarks only.
-    std::map<std::pair<int, int>, int> blk_index;
-    std::vector<std::pair<int, int>> blocks;
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> blk_trip;
-    auto block_of = [&](int i1, int i2) {
-        auto key = std::make_pair(i1, i2);
-        auto it = blk_index.find(key);
-        if (it != blk_index.end()) return it->second;
-        const int bi = (int)blocks.size();
-        blk_index[key] = bi;
-        blocks.push_back(key);
-        blk_trip.emplace_back();
-        return bi;
-    };
-    for (int h = 0; h < nf; ++h) block_of(h, h);
-    if (R > 1) {  // global pattern: free poses observing each landmark of the full window
-        std::vector<std::vector<int32_t>> obs_h(n_pt_g + n_ln_g);
-        for (int e = 0; e < Ep_g; ++e)
-            if (kf_hidx[g->ept_kf[e]] >= 0) obs_h[g->ept_lm[e]].push_back(kf_hidx[g->ept_kf[e]]);
-        for (int e = 0; e < El_g; ++e)
-            if (kf_hidx[g->eln_kf[e]] >= 0) obs_h[n_pt_g + g->eln_lm[e]].push_back(kf_hidx[g->eln_kf[e]]);
-        for (auto &hs : obs_h)
-            for (int a : hs)
-                for (int b : hs)
-                    if (a < b) block_of(a, b);
-    }
-    std::vector<int32_t> lm_edges;
-    for (int l = 0; l < n_lm; ++l) {
-        lm_edges.clear();
-        for (int e = lm_off[l]; e < lm_off[l + 1]; ++e)
-            if (e_hidx[e] >= 0) lm_edges.push_back(e);
-        for (int a : lm_edges)
-            for (int b : lm_edges) {
-                const int i1 = e_hidx[a], i2 = e_hidx[b];
-                if (i1 > i2) continue;
-                blk_trip[block_of(i1, i2)].push_back({a, b});
-            }
-    }
-    // envelope (first block column per block row) and bandwidth
+    // Reduced-camera block pattern: the envelope of the lower triangle. first_blk[i2] = the lowest
+    // free pose sharing a landmark with free pose i2, over the WHOLE window on every rank (the
+    // all-reduced value array must have one layout). Blocks are indexed densely within the
+    // envelope in (i2, i1) order; Schur triples (e1 at pose i1 <= e2 at pose i2, same landmark,
+    // local landmarks only) are counting-sorted by block, landmark order inside a block.
     std::vector<int32_t> first_blk(nf);
     for (int h = 0; h < nf; ++h) first_blk[h] = h;
-    for (auto &bk : blocks) first_blk[bk.second] = std::min(first_blk[bk.second], bk.first);
+    {
+        std::vector<int32_t> lmin(n_pt_g + n_ln_g, INT32_MAX);
+        for (int e = 0; e < Ep_g; ++e) {
+            const int h = kf_hidx[g->ept_kf[e]];
+            if (h >= 0) lmin[g->ept_lm[e]] = std::min(lmin[g->ept_lm[e]], h);
+        }
+        for (int e = 0; e < El_g; ++e) {
+            const int h = kf_hidx[g->eln_kf[e]];
+            if (h >= 0) lmin[n_pt_g + g->eln_lm[e]] = std::min(lmin[n_pt_g + g->eln_lm[e]], h);
+        }
+        for (int e = 0; e < Ep_g; ++e) {
+            const int h = kf_hidx[g->ept_kf[e]];
+            if (h >= 0) first_blk[h] = std::min(first_blk[h], lmin[g->ept_lm[e]]);
+        }
+        for (int e = 0; e < El_g; ++e) {
+            const int h = kf_hidx[g->eln_kf[e]];
+            if (h >= 0) first_blk[h] = std::min(first_blk[h], lmin[n_pt_g + g->eln_lm[e]]);
+        }
+    }
     int bw = 0;
     for (int h = 0; h < nf; ++h) bw = std::max(bw, h - first_blk[h]);
     // PLBA_FORCE_DENSE=1 (diagnostics only) routes a narrow envelope through the dense path.
     const char *force_dense = getenv("PLBA_FORCE_DENSE");
     const bool band_mode = bw <= kBandMax && !(force_dense && force_dense[0] == '1');
-    if (band_mode) {  // every envelope block is written each trial (zeros where no landmark couples)
-        for (int i2 = 0; i2 < nf; ++i2)
-            for (int i1 = first_blk[i2]; i1 < i2; ++i1) {
-                auto key = std::make_pair(i1, i2);
-                if (!blk_index.count(key)) {
-                    blk_index[key] = (int)blocks.size();
-                    blocks.push_back(key);
-                    blk_trip.emplace_back();
-                }
-            }
+    std::vector<int64_t> blk_base(nf + 1, 0);
+    for (int h = 0; h < nf; ++h) blk_base[h + 1] = blk_base[h] + (h - first_blk[h] + 1);
+    if (blk_base[nf] > INT32_MAX / 64) {
+        ctx->set_error("reduced camera envelope too large (%lld blocks)", (long long)blk_base[nf]);
+        return PLBA_E_INVALID;
     }
-    const int nblk = (int)blocks.size();
+    const int nblk = (int)blk_base[nf];
     std::vector<int32_t> blk_i1(nblk), blk_i2(nblk), blk_off(nblk + 1, 0), trip;
-    {
-        // order blocks by (i2, i1) for locality; triples keep landmark order
-        std::vector<int> ord(nblk);
-        std::iota(ord.begin(), ord.end(), 0);
-        std::sort(ord.begin(), ord.end(), [&](int a, int b) {
-            return blocks[a].second != blocks[b].second ? blocks[a].second < blocks[b].second
-                                                        : blocks[a].first < blocks[b].first;
-        });
-        size_t tot = 0;
-        for (auto &v : blk_trip) tot += v.size();
-        trip.reserve(tot * 2);
-        for (int k = 0; k < nblk; ++k) {
-            int b = ord[k];
-            blk_i1[k] = blocks[b].first;
-            blk_i2[k] = blocks[b].second;
-            for (auto &t : blk_trip[b]) { trip.push_back(t.first); trip.push_back(t.second); }
-            blk_off[k + 1] = (int32_t)(trip.size() / 2);
+    for (int h = 0; h < nf; ++h)
+        for (int i1 = first_blk[h]; i1 <= h; ++i1) {
+            const int b = (int)(blk_base[h] + (i1 - first_blk[h]));
+            blk_i1[b] = i1;
+            blk_i2[b] = h;
         }
-        ctx->n_triples = tot;
+    {
+        auto for_pairs = [&](auto &&f) {
+            for (int l = 0; l < n_lm; ++l)
+                for (int a = lm_off[l]; a < lm_off[l + 1]; ++a) {
+                    const int i1 = e_hidx[a];
+                    if (i1 < 0) continue;
+                    for (int b = lm_off[l]; b < lm_off[l + 1]; ++b) {
+                        const int i2 = e_hidx[b];
+                        if (i2 < i1) continue;
+                        f(a, b, (int)(blk_base[i2] + (i1 - first_blk[i2])));
+                    }
+                }
+        };
+        for_pairs([&](int, int, int blk) { blk_off[blk + 1]++; });
+        for (int k = 0; k < nblk; ++k) blk_off[k + 1] += blk_off[k];
+        trip.resize(2 * (size_t)blk_off[nblk]);
+        std::vector<int32_t> pos(blk_off.begin(), blk_off.end() - 1);
+        for_pairs([&](int a, int b, int blk) {
+            const size_t t = (size_t)pos[blk]++;
+            trip[2 * t] = a;
+            trip[2 * t + 1] = b;
+        });
+        ctx->n_triples = (size_t)blk_off[nblk];
     }
+    mark("blocks + triples");
     // chunks of <= kChunk triples, never spanning two blocks
     std::vector<int32_t> ch_blk, ch_off, blk_ch(nblk + 1, 0);
     for (int k = 0; k < nblk; ++k) {
@@ -566,6 +624,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         tile_last[K] = last;
     }
 
+    mark("chunks + envelope");
     // ---- device allocation
     Dev &d = ctx->d;
     d.n_kf = n_kf; d.n_pt = n_pt; d.n_ln = n_ln; d.n_lm = n_lm; d.Ep = Ep; d.El = El; d.E = E;
@@ -615,13 +674,13 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         for (int k = 0; k < 4; ++k)
             X[(size_t)(n_pt + l) * 4 + k] = g->ln_orth[4 * (size_t)(lm_gpos[n_pt + l] - n_pt_g) + k];
 
-    int rc = 0;
-#define ALLOC(p, n_)        \
-    rc = ctx->alloc(p, n_); \
-    if (rc) return rc
-#define UPLOAD(p, v)            \
-    rc = upload_vec(ctx, p, v); \
-    if (rc) return rc
+    std::vector<int32_t> h_kf(bcr ? nf : 0, 0);
+    for (int k = 0; k < n_kf && bcr; ++k)
+        if (kf_hidx[k] >= 0) h_kf[kf_hidx[k]] = k;
+    // every device array of the window, carved from the arena (commit_plan assigns the pointers)
+#define ALLOC(p, n_) ctx->alloc(p, (size_t)(n_))
+#define ZALLOC(p, n_) ctx->alloc(p, (size_t)(n_), nullptr, true)
+#define UPLOAD(p, v) ctx->alloc(p, (v).size(), (v).data())
     UPLOAD(d.T_init, T);
     UPLOAD(d.Tb[0], T);
     ALLOC(d.Tb[1], T.size());
@@ -636,7 +695,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.e_hidx, e_hidx);
     UPLOAD(d.e_obs, e_obs);
     UPLOAD(d.e_info, e_info);
-    ALLOC(d.e_level, E);
+    ZALLOC(d.e_level, E);
     ALLOC(d.e_active, E);
     UPLOAD(d.lm_off, lm_off);
     ALLOC(d.lm_active, n_lm);
@@ -645,25 +704,15 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.A, (size_t)E * 12);
     ALLOC(d.cvec, (size_t)E * 2);
     ALLOC(d.B, (size_t)E * 8);
-    ALLOC(d.chi2_last, E);
-    // Hpp | b_p | χ² | active | landmark max per rank: one array, all-reduced when sharded
+    ZALLOC(d.chi2_last, E);
+    // Hpp | b_p | #active edges | χ² | active | landmark max per rank: one array, all-reduced when sharded
     ALLOC(d.red_iter, (size_t)nf * 43 + 2 + R);
-    d.Hpp = d.red_iter;
-    d.bp = d.red_iter + (size_t)nf * 36;
-    d.pact = d.red_iter + (size_t)nf * 42;
-    if (sharded) {
-        ALLOC(d.red_iter_loc, (size_t)nf * 43 + 2 + R);
-    } else {
-        d.red_iter_loc = d.red_iter;
-    }
-    d.Hpp_w = d.red_iter_loc;
-    d.bp_w = d.red_iter_loc + (size_t)nf * 36;
-    d.pact_w = d.red_iter_loc + (size_t)nf * 42;
+    if (sharded) ALLOC(d.red_iter_loc, (size_t)nf * 43 + 2 + R);
     ALLOC(d.Hll, (size_t)n_lm * 10);
     ALLOC(d.bl, (size_t)n_lm * 4);
     ALLOC(d.Z, (size_t)E * 8);
     ALLOC(d.q, (size_t)E * 2);
-    ALLOC(d.xl, (size_t)n_lm * 4);
+    ZALLOC(d.xl, (size_t)n_lm * 4);
     UPLOAD(d.blk_i1, blk_i1);
     UPLOAD(d.blk_i2, blk_i2);
     UPLOAD(d.blk_off, blk_off);
@@ -675,33 +724,32 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.ch_part, (size_t)std::max(nch, 1) * 42);
     ALLOC(d.Ad, band_mode ? 1 : (size_t)n * n);
     UPLOAD(d.first_blk, first_blk);
-    ALLOC(d.Bd, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
+    // band blocks outside the envelope (w > i - first_blk[i]) are never assembled and must
+    // read as zero: the band kernels sweep all BW block columns of every row
+    ZALLOC(d.Bd, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
     ALLOC(d.Lband, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
     ALLOC(d.Kinv, (size_t)nf * 36);
     ALLOC(d.zb, (size_t)nf * 6);
     if (twisted) {
-        ALLOC(d.Bd2, (size_t)nf * (bw + 1) * 36);
+        ZALLOC(d.Bd2, (size_t)nf * (bw + 1) * 36);
         ALLOC(d.bs2, (size_t)nf * 6);
         ALLOC(d.Lband2, (size_t)nf * (bw + 1) * 36);
         ALLOC(d.Kinv2, (size_t)nf * 36);
         ALLOC(d.zb2, (size_t)nf * 6);
         ALLOC(d.tw_sep, 2 * ((size_t)bw * (bw + 1) * 36 + (size_t)bw * 6));
-        ALLOC(d.tw_fail, 2);
-        ALLOC(d.tw_count, 1);
+        ZALLOC(d.tw_fail, 2);
+        ZALLOC(d.tw_count, 1);
     }
-    if (bcr) {
+    if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate
         ALLOC(d.bcr_pub, (size_t)d.bcr_N * bcr_pub_doubles(bw));
         ALLOC(d.bcr_x, (size_t)d.bcr_N * bcr_xrec(bw));
-        std::vector<int32_t> h_kf(nf, 0);
-        for (int k = 0; k < n_kf; ++k)
-            if (kf_hidx[k] >= 0) h_kf[kf_hidx[k]] = k;
         UPLOAD(d.h_kf, h_kf);
-        ALLOC(d.bcr_flag, 2 * (size_t)d.bcr_N);
-        ALLOC(d.bcr_ctl, 4);
-        ALLOC(d.bcr_stamps, (size_t)d.bcr_N * kBcrStamps);
+        ZALLOC(d.bcr_flag, 2 * (size_t)d.bcr_N);
+        ZALLOC(d.bcr_ctl, 4);
+        ZALLOC(d.bcr_stamps, (size_t)d.bcr_N * kBcrStamps);
     }
     ALLOC(d.bs, n);
-    ALLOC(d.xp, n);
+    ZALLOC(d.xp, n);
     ALLOC(d.Wbuf, (size_t)std::max(n, 1) * kTile);
     UPLOAD(d.tile_first, tile_first);
     UPLOAD(d.tile_last, tile_last);
@@ -712,8 +760,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_lm, std::max(d.n_lms_blocks, 1));
     ALLOC(d.part_lms, d.n_lms_blocks);
     d.n_ps = std::max(d.n_kf_blocks, d.bcr_N);
-    ALLOC(d.part_ps, d.n_ps);
-    ALLOC(d.ctrl, 1);
+    ZALLOC(d.part_ps, d.n_ps);
+    ZALLOC(d.ctrl, 1);
     ALLOC(d.trace, kTraceCap);
     ALLOC(ctx->d_depth, Ep);
     ALLOC(d.red_rcs, (size_t)nblk * 36 + (size_t)nf * 6);
@@ -728,39 +776,32 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ALLOC(d.gat, (size_t)(n_pt_g + n_ln_g) * 4 + 3 * (size_t)(Ep_g + El_g));
     }
 #ifdef PLBA_STAMPS
-    ALLOC(d.stamps, 17 * 8);
-    PLBA_CHECK(hipMemset(d.stamps, 0, 17 * 8 * sizeof(unsigned long long)));
+    ZALLOC(d.stamps, 17 * 8);
 #endif
 #undef ALLOC
+#undef ZALLOC
 #undef UPLOAD
+    mark("host arrays staged");
+    int rc = ctx->commit_plan();
+    if (rc) return rc;
+    d.Hpp = d.red_iter;
+    d.bp = d.red_iter + (size_t)nf * 36;
+    d.pact = d.red_iter + (size_t)nf * 42;
+    if (!sharded) d.red_iter_loc = d.red_iter;
+    d.Hpp_w = d.red_iter_loc;
+    d.bp_w = d.red_iter_loc + (size_t)nf * 36;
+    d.pact_w = d.red_iter_loc + (size_t)nf * 42;
     if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)band_lds_bytes(bw, nf)));
-    if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate
-        PLBA_CHECK(hipFuncSetAttribute(bcr_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bcr_lds_bytes(bw)));
-        PLBA_CHECK(hipMemset(d.bcr_flag, 0, 2 * sizeof(uint32_t) * (size_t)d.bcr_N));
-        PLBA_CHECK(hipMemset(d.bcr_ctl, 0, 4 * sizeof(uint32_t)));
-    }
+    if (bcr) PLBA_CHECK(hipFuncSetAttribute(bcr_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bcr_lds_bytes(bw)));
     if (d.cl) {  // the column-lane kernel's LDS grows with nf (x_p staging of the two-sided variant)
         const void *k = cl_kernel_impl(bw, twisted, std::make_integer_sequence<int, kClMaxBW + 1>{});
         PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, twisted)));
     }
-    if (twisted) {
+    if (twisted)
         PLBA_CHECK(hipFuncSetAttribute(twisted_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)twisted_lds_bytes(bw, nf)));
-        PLBA_CHECK(hipMemset(d.Bd2, 0, sizeof(double) * (size_t)nf * (bw + 1) * 36));
-        PLBA_CHECK(hipMemset(d.tw_count, 0, sizeof(int32_t)));
-        PLBA_CHECK(hipMemset(d.tw_fail, 0, 2 * sizeof(int32_t)));
-    }
-    // (zero-sized arrays are allocated with one element: clear exactly what alloc() gave)
-    // band blocks outside the envelope (w > i - first_blk[i]) are never assembled and must
-    // read as zero: the band kernel sweeps all BW block columns of every row
-    if (band_mode) PLBA_CHECK(hipMemset(d.Bd, 0, sizeof(double) * (size_t)nf * (bw + 1) * 36));
-    PLBA_CHECK(hipMemset(d.e_level, 0, std::max(E, 1)));
-    PLBA_CHECK(hipMemset(d.xp, 0, sizeof(double) * std::max(n, 1)));
-    PLBA_CHECK(hipMemset(d.xl, 0, sizeof(double) * std::max((size_t)n_lm * 4, (size_t)1)));
-    PLBA_CHECK(hipMemset(d.chi2_last, 0, sizeof(double) * std::max(E, 1)));
-    PLBA_CHECK(hipMemset(d.ctrl, 0, sizeof(Ctrl)));
-    PLBA_CHECK(hipDeviceSynchronize());
+    mark("alloc + copy + memset");
     ctx->uploaded = true;
     ctx->initialized = false;
     ctx->cur = 0;
@@ -871,9 +912,13 @@ int capture_steps(plba_ctx *ctx, int nsteps, hipGraph_t &graph, hipGraphExec_t &
 }
 int capture_step(plba_ctx *ctx) {
     if (ctx->step_exec) return PLBA_OK;
+    const auto t0 = std::chrono::steady_clock::now();
     int rc = capture_steps(ctx, 1, ctx->step_graph, ctx->step_exec);
     for (int i = 0; i < plba_ctx::kMultiLevels && !rc; ++i)
         rc = capture_steps(ctx, 2 << i, ctx->multi_graph[i], ctx->multi_exec[i]);
+    if (env_flag("PLBA_TIMING"))
+        fprintf(stderr, "[plba upload] %-24s %8.3f ms\n", "graph capture",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     return rc;
 }
 // launch n replays of the step as the binary decomposition of n over the captured graphs
@@ -1055,6 +1100,8 @@ int plba_destroy(plba_ctx *ctx) {
     (void)hipSetDevice(ctx->opts.device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->free_all();
+    if (ctx->arena) (void)hipFree(ctx->arena);
+    if (ctx->staging) (void)hipHostFree(ctx->staging);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
     if (ctx->comm.hbuf) (void)hipHostFree(ctx->comm.hbuf);

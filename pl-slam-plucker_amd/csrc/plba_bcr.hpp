@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
         double *red = pv + 96;            // [kBcrParts][S]
         double *ps = red + kBcrParts * S;  // [BW][24] Tcw | b_p | previous x_p of this row's poses, λ
         __shared__ uint32_t s_epoch;
-        __shared__ int s_fail, s_last;
+        __shared__ int s_fail;
         __shared__ double s_sum[NT / 64];
         __shared__ int s_kf[BW + 1];
         const int tid = threadIdx.x, m = blockIdx.x, N = d.bcr_N, nf = d.nf;

@@ -132,6 +132,7 @@ def test_column_lane_factorisation_bandwidths(solver, monkeypatch, tmax, n_kf):
     g = synth.generate("C1L", n_kf=n_kf, n_pt=30 * n_kf, n_ln=6 * n_kf, seed=300 + tmax + n_kf,
                        track_min=2, track_max=tmax, fixed_frac=0.1)
     ref = oa.lba_plucker(g)
+    monkeypatch.setenv("PLBA_FACTOR", "cl")
     solver.upload(g)
     st = solver.structure_stats()
     assert st["banded"] == 1 and st["column_lane"] == 1 and st["bw"] <= 9, st
@@ -143,6 +144,7 @@ def test_column_lane_factorisation_bandwidths(solver, monkeypatch, tmax, n_kf):
     assert solver.structure_stats()["column_lane"] == 0
     old = solver.lba_plucker()
     monkeypatch.delenv("PLBA_NO_CL")
+    monkeypatch.delenv("PLBA_FACTOR")
     _check(old, ref)
     assert np.abs(cl["kf_Tcw"] - old["kf_Tcw"]).max() < 1e-9
 
