@@ -9,12 +9,13 @@ wall time. Workload (N=1): config C3 = 100 KF / 20k points / 4k lines (BASELINE.
 configs[2], the window north_star quotes its ≥50x target on).
 
 Multi-GPU (`--gpus N`, launched by torch.distributed.run), two modes:
-  --mode replicas (default)  every rank solves its own independent C3 window (different seed):
+  --mode shard (default for N > 1)  ONE window split over the ranks by landmark:
+                             BASELINE.json configs[3] (C4, 400 KF, "sharded 4×MI355X") for N = 2, 4
+                             and configs[4] (C5, 1000 KF, 8×MI355X) for N = 8; partial reduced
+                             camera systems summed with RCCL all-reduces inside the captured step
+                             graph (strong scaling); `--transport host` rehearses it with gloo.
+  --mode replicas            every rank solves its own independent C3 window (different seed):
                              independent LBA windows need no data-path collective (weak scaling).
-  --mode shard               ONE window (default C4) split over the ranks by landmark
-                             (SURVEY.md §8e), partial reduced camera systems summed with RCCL
-                             all-reduces inside the captured step graph (strong scaling);
-                             `--transport host` rehearses it with gloo on one GPU.
 The barrier and max-over-ranks timing use torch.distributed in both.
 
 Extra JSON objects:
@@ -52,32 +53,52 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-runs", type=int, default=5)
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK (multi-rank rehearsal on 1 GPU)")
-    p.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
+    p.add_argument("--mode", choices=["replicas", "shard"], default=None,
+                   help="default: replicas at N=1 (one C3 window), shard for N>1")
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="--mode shard all-reduce transport")
     return p.parse_args()
 
 
+def cpu_model() -> str:
+    """`lscpu` model name of this host (reported next to every CPU number)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg: str, runs: int):
-    """Time the CPU oracle (refcpu, -O3 -march=native, 1 thread) on the same window."""
+    """Time the CPU oracle (refcpu, -O3 -march=native, 1 thread) on the same window, pinned to one
+    core (the `taskset -c <cpu>` of BASELINE.md §2, via sched_setaffinity on this process)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import ctypes as C  # noqa: F401
     import oracle_api as oa
     subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-s", "native"], check=True)
     oa.ORACLE_SO = os.path.join(ROOT, "oracle", "librefcpu_native.so")
     g = synth.generate(cfg)
-    oa.lba_plucker(g)  # warm
-    ms, iters = [], []
-    for _ in range(runs):
-        r = oa.lba_plucker(g)
-        ms.append(r["solve_ms"])
-        iters.append(int(r["iters"][0] + r["iters"][1]))
+    prev = os.sched_getaffinity(0)
+    core = min(prev)
+    os.sched_setaffinity(0, {core})
+    try:
+        oa.lba_plucker(g)  # warm
+        ms, iters = [], []
+        for _ in range(runs):
+            r = oa.lba_plucker(g)
+            ms.append(r["solve_ms"])
+            iters.append(int(r["iters"][0] + r["iters"][1]))
+    finally:
+        os.sched_setaffinity(0, prev)
     med = statistics.median(ms)
     it = iters[0]
     return dict(value=it / (med / 1e3), unit="LM iterations/s", cores=1, kind="port",
+                cpu_model=cpu_model(), pinned_core=core, host_cpus=os.cpu_count(),
                 final_chi2=[float(r["chi2"][0]), float(r["chi2"][1])],
                 sample=f"{cfg} window ({g.n_kf} KF, {g.n_pt} pts, {g.n_ln} lines, {g.n_ept + g.n_eln} edges), "
                        f"full 2-stage LBA ({it} outer iterations), 1 warm + {runs} timed runs, median "
-                       f"{med:.1f} ms/LBA; oracle/refcpu.cpp -O3 -march=native, 1 thread",
+                       f"{med:.1f} ms/LBA; oracle/refcpu.cpp (g2o-structured restatement) -O3 -march=native, "
+                       f"1 thread pinned to core {core}",
                 ms_per_lba=med)
 
 
@@ -93,9 +114,11 @@ def main():
         dist.init_process_group("gloo")
     from plba.lib import Solver
 
+    if a.mode is None:
+        a.mode = "shard" if world > 1 else "replicas"
     shard = a.mode == "shard"
-    if shard and a.config == "C3" and "--config" not in sys.argv:
-        a.config = "C4"
+    if shard and "--config" not in sys.argv:
+        a.config = "C5" if world >= 8 else "C4"   # BASELINE.json configs[4] / configs[3]
     base_seed = synth.CONFIGS[a.config][3]
     dev = local if a.device is None else a.device
     if shard:  # one window for all ranks
@@ -128,6 +151,7 @@ def main():
     s.L.plba_enable_kernel_timing(s.ctx, 1)
     r = step()
     ktimes = s.kernel_times()
+    info = s.structure_stats()
     s.L.plba_enable_kernel_timing(s.ctx, 0)
 
     s.synchronize()
@@ -156,19 +180,38 @@ def main():
             dist.all_reduce(ti, op=dist.ReduceOp.SUM)
             tot_iters = int(ti.item())
 
+    # End-to-end LBA call on a NEW window of the same config: upload (host
+    # marshalling + one pinned copy) + step-graph capture + the two-stage solve + download of every
+    # output, as the drop-in use pays it per call; the second of two windows is reported (the
+    # first pays one-time arena / code-object costs). Outside the timed region.
+    e2e = []
+    for k in range(2):
+        g2 = synth.generate(a.config, seed=base_seed + 7919 * (k + 1) + 97 * rank)
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        s.upload(g2)
+        t1 = time.perf_counter()
+        r2 = s.lba_plucker(want_outputs=True, with_trace=False)
+        t2 = time.perf_counter()
+        e2e.append(dict(end_to_end_ms=(t2 - t0) * 1e3, upload_ms=(t1 - t0) * 1e3,
+                        solve_and_download_ms=(t2 - t1) * 1e3, solve_ms=float(r2["solve_ms"])))
+
     if rank == 0:
         # dominant kernel by device time in the instrumented step
         name, (kms, nl) = max(((k, v) for k, v in ktimes.items() if v[1] > 0), key=lambda kv: kv[1][0])
         avg_ms = kms / max(nl, 1)
-        info = s.structure_stats()
-        alg = kernel_bytes(g, name, info)
-        achieved = alg / (avg_ms * 1e-3) / 1e9
         # rocprofv3 names the banded factorisation by its template (k_rcs_factor_band<BW>)
         prof_name = name
         if name == "k_rcs_factor" and info.get("banded"):
-            prof_name = "k_rcs_factor_twisted" if info.get("twisted") else "k_rcs_factor_band"
-            if info.get("column_lane"):
-                prof_name += "_cl"
+            if info.get("bcr_rows"):
+                prof_name = "k_rcs_factor_bcr"
+            else:
+                prof_name = "k_rcs_factor_twisted" if info.get("twisted") else "k_rcs_factor_band"
+                if info.get("column_lane"):
+                    prof_name += "_cl"
+        alg = kernel_bytes(g, prof_name if prof_name == "k_rcs_factor_bcr" else name, info)
+        achieved = alg / (avg_ms * 1e-3) / 1e9
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
         traffic = None
         if os.path.exists(pmc_path):
@@ -180,7 +223,7 @@ def main():
         for k, (ms_k, n_k) in ktimes.items():
             if n_k <= 0:
                 continue
-            b = kernel_bytes(g, k, info)
+            b = kernel_bytes(g, "k_rcs_factor_bcr" if (k == "k_rcs_factor" and info.get("bcr_rows")) else k, info)
             us = ms_k / n_k * 1e3
             per_kernel[k] = {"us_per_launch": round(us, 2), "launches_per_lba": n_k,
                              "alg_bytes": int(b), "GBs": round(b / (us * 1e-6) / 1e9, 1) if b else None}
@@ -208,6 +251,9 @@ def main():
                 "trials_per_lba": trials / a.steps,
                 "ms_per_lm_iteration": dt / max(iters, 1) * 1e3,
                 "upload_ms": upload_ms,
+                "end_to_end": e2e[-1],
+                "factorisation": ("block cyclic reduction over %d super-rows" % info["bcr_rows"] if info.get("bcr_rows")
+                                  else ("two-sided column-lane band LDLT" if info.get("twisted") else "band LDLT")),
                 "parallelism": (f"landmark-sharded window over {world} GPU(s)" if shard
                                 else f"{world} independent windows (1 per GPU)"),
             },
@@ -222,10 +268,9 @@ def main():
                 "alg_bytes_per_launch": alg,
                 "avg_launch_us": avg_ms * 1e3,
                 "launches_per_lba": nl,
-                "note": ("latency-bound banded LDLᵀ of the reduced camera system: a serial chain of 6x6 "
-                         "block pivots (column-lane Gauss–Jordan on one wave per segment, two segments "
-                         "meeting at a separator) + back substitution + pose update; bytes/launch are tiny "
-                         "by nature — see DESIGN.md §4"),
+                "note": ("latency-bound factorisation of the reduced camera system (a serial chain of 6x6 "
+                         "pivot blocks or of dense super-row eliminations) + back substitution + pose update; "
+                         "bytes/launch are tiny by nature — see DESIGN.md §4"),
             },
             "iteration_roofline": {
                 "alg_bytes_per_iter": iter_bytes,

@@ -56,6 +56,16 @@ def kernel_bytes(g: Graph, name: str, st: dict) -> float:
         # current poses in, trial poses out, b_p in
         return (nf * (bw + 1) * blk + nf * 6 * F + nf * bw * blk + nf * (36 + 6 + 6) * F
                 + g.n_kf * (12 + 12) * F + nf * 6 * F)
+    if name == "k_rcs_factor_bcr":
+        # block cyclic reduction over N = ceil(nf/bw) super-rows of S = 6·bw: band + b_s in once;
+        # every non-root super-row writes one Schur record (36·NG Gram-tile values, NG = lower
+        # triangle of (2bw+1)² blocks minus the (b,b) corner) read by its two neighbours; each
+        # solution record (S) written once and read by up to two neighbours; x_p and the poses
+        S = 6 * bw
+        N = -(-nf // max(bw, 1))
+        NG = (2 * bw + 1) * (2 * bw + 2) // 2 - 1
+        return (nf * (bw + 1) * blk + nf * 6 * F + (N - 1) * 36 * NG * F * 3 + N * S * F * 3
+                + nf * 6 * F + g.n_kf * (12 + 12) * F + nf * 6 * F)
     if name == "k_pose_update":
         return g.n_kf * (12 + 12) * F + nf * 12 * F
     if name == "k_lm_solve":
