@@ -597,13 +597,17 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     }
     mark("blocks + triples");
     // chunks of <= kChunk triples, never spanning two blocks
+    // (at least one chunk per block, possibly empty: the last chunk of a block to finish
+    // assembles it, so every envelope block — zero ones included — is written each trial)
     std::vector<int32_t> ch_blk, ch_off, blk_ch(nblk + 1, 0);
     for (int k = 0; k < nblk; ++k) {
         blk_ch[k] = (int32_t)ch_blk.size();
-        for (int t = blk_off[k]; t < blk_off[k + 1]; t += kChunk) {
+        int t = blk_off[k];
+        do {
             ch_blk.push_back(k);
             ch_off.push_back(t);
-        }
+            t += kChunk;
+        } while (t < blk_off[k + 1]);
     }
     blk_ch[nblk] = (int32_t)ch_blk.size();
     ch_off.push_back(blk_off[nblk]);
@@ -759,6 +763,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * kPP);
     ALLOC(d.part_lm, std::max(d.n_lms_blocks, 1));
     ALLOC(d.part_lms, d.n_lms_blocks);
+    d.fold = sharded ? 0 : 1;
+    ZALLOC(d.cnt, 2 + (size_t)nblk);
     d.n_ps = std::max(d.n_kf_blocks, d.bcr_N);
     ZALLOC(d.part_ps, d.n_ps);
     ZALLOC(d.ctrl, 1);
@@ -872,7 +878,8 @@ int launch_step(plba_ctx *ctx) {
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
             COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);
         }
-        LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
+        if (!(d.fold && d.nch > 0))  // (folded into the last chunk of each block otherwise)
+            LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
         if (d.band_mode) LAUNCH(K_FACTOR, launch_band(d, s));
         else LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
     }
@@ -885,7 +892,8 @@ int launch_step(plba_ctx *ctx) {
         LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide_pack, dim3(1), dim3(kBlock), 0, s, d));
         COMM(d.red_dec_loc, d.red_dec, 2);
     }
-    LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d));
+    if (!(d.fold && d.n_lm > 0))  // (folded into the last k_lm_solve workgroup otherwise)
+        LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d));
     return PLBA_OK;
 }
 

@@ -55,12 +55,6 @@ __host__ __device__ constexpr size_t bcr_pub_doubles(int bw) { return (size_t)36
 // solution record of a super-row: x (6 bw) + failure word (propagated down the back substitution)
 __host__ __device__ constexpr int bcr_xrec(int bw) { return 6 * bw + 2; }
 
-__device__ __forceinline__ double ld_sc1(const double *p) {
-    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double *p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // one lane: relaxed poll until the flag carries `epoch`; bounded (~0.3 s), timeout -> *err = 1
 __device__ __forceinline__ bool bcr_poll(uint32_t *flag, uint32_t epoch, int32_t *err) {
     for (uint32_t spins = 0;; ++spins) {

@@ -122,6 +122,9 @@ struct Dev {
     double *part_lm, *part_lms;         // [n_lms_blocks] trial χ² partials, scale partials (k_lm_solve)
     double *part_ps;                    // [n_ps] pose part of Σx(λx+b) (one slot per factorisation workgroup)
     int32_t n_ps;                       // max(n_kf_blocks, bcr_N)
+    int32_t fold;                       // 1: k_rcs_finalize / k_decide run as the tails of the
+                                        //    preceding launch (last arriver); 0 when sharded
+    int32_t *cnt;                       // [2 + nblk] arrival counters: lm_solve, (spare), per RCS block
     int32_t *h_kf;                      // [nf] keyframe of each free-pose Hessian index
     Ctrl *ctrl;
     plba_iter_trace *trace;             // [kTraceCap] per-iteration records written by k_decide
@@ -197,6 +200,31 @@ __device__ __forceinline__ double block_max(double v, double *sh) {
     return r;
 }
 __device__ __forceinline__ bool is_point_lm(const Dev &d, int lm) { return lm < d.n_pt; }
+
+// ---------------------------------------------------------------- in-launch hand-offs
+// Write-through (sc1) stores / loads: MI355X_MICROARCH.md "Valid forms" row 1 — data stored sc1,
+// every storing wave drained, one lane per workgroup adds to an agent-scope counter, the
+// workgroup whose add returns total-1 is last and reads the others' data with sc1 loads.
+__device__ __forceinline__ double ld_sc1(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Every thread calls it after its sc1 stores; true in the last of `total` arriving workgroups,
+// which resets the counter for the next launch (exactly `total` arrivals per launch).
+__device__ __forceinline__ bool arrive_last(int32_t *counter, int32_t total) {
+    __shared__ int s_last_arrival;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int32_t old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last_arrival = old == total - 1 ? 1 : 0;
+        if (s_last_arrival) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return s_last_arrival != 0;
+}
 
 #ifdef PLBA_STAMPS
 #define STAMP(slot)                                                                         \
@@ -546,6 +574,37 @@ __global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
 }
 
 // ---------------------------------------------------------------- reduced camera system
+// one entry of block b: e < 36 the 6x6 value (Hpp + λI on the diagonal minus Σ chunks), 36..41
+// the right-hand side b_s = b_p - Σ A_eᵀq_e (diagonal blocks only)
+__device__ __forceinline__ void rcs_finalize_entry(const Dev &d, int b, int e, double sacc) {
+    const int i1 = d.blk_i1[b], i2 = d.blk_i2[b];
+    const bool diag = i1 == i2;
+    if (e >= 36 && !diag) return;
+    const int n = d.n;
+    if (e >= 36) {
+        const double v = d.bp[(size_t)i1 * 6 + (e - 36)] - sacc;
+        d.bs[6 * i1 + (e - 36)] = v;
+        if (d.twisted) d.bs2[6 * (d.nf - 1 - i1) + (e - 36)] = v;
+        return;
+    }
+    const int r = e / 6, c = e % 6;
+    if (diag) {
+        double h = d.Hpp[(size_t)i1 * 36 + e] - sacc;
+        // a free pose with no active edge is not in g2o's system (SparseOptimizer activation,
+        // SURVEY.md §8 A13); its all-zero block row becomes I (x = 0 exactly) instead of λI,
+        // which would be a zero pivot at λ = 0
+        if (r == c) h += d.pact[i1] != 0.0 ? d.ctrl->lambda : 1.0;
+        if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
+        else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
+        if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1)) * 36 + e] = h;
+    } else {
+        if (d.band_mode) d.Bd[((size_t)i2 * (d.bw + 1) + (i2 - i1)) * 36 + c * 6 + r] = -sacc;
+        else d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -sacc;
+        // reversed row nf-1-i1 holds block (i1, i2) = (i1, i1 + w) in its natural orientation
+        if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1) + (i2 - i1)) * 36 + r * 6 + c] = -sacc;
+    }
+}
+
 // Chunked reduced-camera assembly, pass 1: one wave per chunk of <= kChunk triples of one
 // block; each lane accumulates A₁ᵀ(Z₁Z₂ᵀ)A₂ (36) and, for self-triples of a diagonal block,
 // A_eᵀ q_e (6); the wave reduces through LDS in fixed lane order (deterministic).
@@ -608,7 +667,20 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
     if (lane < 42) {
         double sacc = 0.0;
         for (int l = 0; l < 64; ++l) sacc += red[l][lane];
-        d.ch_part[(size_t)ch * 42 + lane] = sacc;
+        st_sc1(d.ch_part + (size_t)ch * 42 + lane, sacc);
+    }
+    // the last chunk of block b to arrive assembles the block (the k_rcs_finalize entry work)
+    if (d.fold && arrive_last(d.cnt + 2 + b, d.blk_ch[b + 1] - d.blk_ch[b]) && lane < 42) {
+        double sacc = 0.0;
+        const int c1 = d.blk_ch[b + 1];
+        for (int c0 = d.blk_ch[b]; c0 < c1; c0 += 4) {  // 4 partials in flight, summed in chunk order
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = c0 + u < c1 ? ld_sc1(d.ch_part + (size_t)(c0 + u) * 42 + lane) : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sacc += v[u];
+        }
+        rcs_finalize_entry(d, b, lane, sacc);
     }
 }
 
@@ -633,36 +705,13 @@ __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
     const int gid = blockIdx.x * kBlock + threadIdx.x;
     const int b = gid / 42, e = gid % 42;
     if (b >= d.nblk) return;
-    const int i1 = d.blk_i1[b], i2 = d.blk_i2[b];
-    const bool diag = i1 == i2;
-    if (e >= 36 && !diag) return;
+    const int i1 = d.blk_i1[b];
+    if (e >= 36 && i1 != d.blk_i2[b]) return;
     double sacc = 0.0;
     if (d.sharded) sacc = e < 36 ? d.red_rcs[(size_t)b * 36 + e] : d.red_rcs[(size_t)d.nblk * 36 + 6 * i1 + (e - 36)];
     else
         for (int c = d.blk_ch[b]; c < d.blk_ch[b + 1]; ++c) sacc += d.ch_part[(size_t)c * 42 + e];
-    const int n = d.n;
-    if (e >= 36) {
-        const double v = d.bp[(size_t)i1 * 6 + (e - 36)] - sacc;
-        d.bs[6 * i1 + (e - 36)] = v;
-        if (d.twisted) d.bs2[6 * (d.nf - 1 - i1) + (e - 36)] = v;
-        return;
-    }
-    const int r = e / 6, c = e % 6;
-    if (diag) {
-        double h = d.Hpp[(size_t)i1 * 36 + e] - sacc;
-        // a free pose with no active edge is not in g2o's system (SparseOptimizer activation,
-        // SURVEY.md §8 A13); its all-zero block row becomes I (x = 0 exactly) instead of λI,
-        // which would be a zero pivot at λ = 0
-        if (r == c) h += d.pact[i1] != 0.0 ? d.ctrl->lambda : 1.0;
-        if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
-        else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
-        if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1)) * 36 + e] = h;
-    } else {
-        if (d.band_mode) d.Bd[((size_t)i2 * (d.bw + 1) + (i2 - i1)) * 36 + c * 6 + r] = -sacc;
-        else d.Ad[(size_t)(6 * i2 + c) + (size_t)(6 * i1 + r) * n] = -sacc;
-        // reversed row nf-1-i1 holds block (i1, i2) = (i1, i1 + w) in its natural orientation
-        if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1) + (i2 - i1)) * 36 + r * 6 + c] = -sacc;
-    }
+    rcs_finalize_entry(d, b, e, sacc);
 }
 
 // oplus of every free pose with x_p (trial state; fixed poses copied), and the pose part of
@@ -1676,6 +1725,87 @@ __device__ __forceinline__ double lm_eval(const Dev &d, const LmEdge &s, const d
     return rho0;
 }
 
+// OptimizationAlgorithmLevenberg trial decision (SURVEY.md §8a A13) + optimize() loop control.
+// Runs as its own launch (sharded windows, windows without landmarks) or as the tail of the last
+// k_lm_solve workgroup; the landmark partials are read with sc1 loads in both cases.
+template <int NT>
+__device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
+    double a = 0.0, b = 0.0;
+    if (!d.sharded) {  // 8 loads of each array in flight per thread; summed in index order
+        constexpr int U = 8;
+        for (int i0 = threadIdx.x; i0 < d.n_lms_blocks; i0 += NT * U) {
+            double va[U], vb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NT;
+                const bool ok = i < d.n_lms_blocks;
+                va[u] = ok ? ld_sc1(d.part_lm + i) : 0.0;
+                vb[u] = ok ? ld_sc1(d.part_lms + i) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                a += va[u];
+                b += vb[u];
+            }
+        }
+    }
+    for (int i = threadIdx.x; i < d.n_ps; i += NT) b += d.part_ps[i];  // poses: replicated
+    double tempChi0 = block_sum<NT>(a, sh);
+    double scale0 = block_sum<NT>(b, sh);
+    if (d.sharded) {  // landmark terms summed over ranks
+        tempChi0 = d.red_dec[0];
+        scale0 += d.red_dec[1];
+    }
+    if (threadIdx.x != 0) return;
+    Ctrl *c = d.ctrl;
+    c->steps += 1;
+    double tempChi = tempChi0;
+    if (!c->solve_ok) tempChi = 1.7976931348623157e308;
+    const double scale = scale0 + 1e-3;
+    const double rho = (c->currentChi - tempChi) / scale;
+    c->tempChi = tempChi;
+    c->scale = scale;
+    c->rho = rho;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        const double sf = fmax(1. / 3., alpha);
+        c->lambda *= sf;
+        c->ni = 2;
+        c->currentChi = tempChi;
+        c->accept = 1;
+        c->qmax += 1;
+    } else {
+        c->lambda *= c->ni;
+        c->ni *= 2;
+        c->accept = 0;
+        if (!isfinite(c->lambda)) c->broke = 1;
+        else c->qmax += 1;
+    }
+    if (c->accept) c->cur ^= 1;  // the trial becomes the current estimate
+    const bool again = !c->broke && rho < 0 && c->qmax < c->max_trials;
+    if (again) return;  // another damped trial of this iteration
+    // end of OptimizationAlgorithmLevenberg::solve(iter)
+    const int terminate = (c->qmax == c->max_trials || rho == 0 || !isfinite(c->lambda)) ? 1 : 0;
+    if (c->ntrace < kTraceCap)
+        d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, c->qmax, terminate, c->chi2_start, c->currentChi,
+                                               c->lambda_start, c->lambda};
+    c->iters_done[c->stage] += 1;
+    c->iter += 1;
+    if (terminate || c->iter >= c->max_iters[c->stage]) {  // optimize() returns
+        c->chi2_final[c->stage] = c->currentChi;
+        if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
+        else c->all_done = 1;
+    } else {
+        c->need_iter = 1;
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
+    TRIAL_GUARD
+    __shared__ double sh[kBlock / 64];
+    decide_body<kBlock>(d, sh);
+}
+
 __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
     TRIAL_GUARD
     __shared__ double sh[kLmsNT / 64];
@@ -1839,9 +1969,11 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
     const double s2 = block_sum<kLmsNT>(sc, sh);
     const double s1 = block_sum<kLmsNT>(chi, sh);
     if (threadIdx.x == 0) {
-        d.part_lms[blockIdx.x] = s2;
-        d.part_lm[blockIdx.x] = s1;
+        st_sc1(d.part_lms + blockIdx.x, s2);
+        st_sc1(d.part_lm + blockIdx.x, s1);
     }
+    // the last workgroup to finish takes the trial decision (k_decide's work)
+    if (d.fold && arrive_last(d.cnt, (int32_t)gridDim.x)) decide_body<kLmsNT>(d, sh);
 }
 // sharded: this rank's trial χ² and landmark scale terms into the all-reduced decision array
 __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
@@ -1855,67 +1987,6 @@ __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
     if (threadIdx.x == 0) {
         d.red_dec_loc[0] = ta;
         d.red_dec_loc[1] = tb;
-    }
-}
-
-// OptimizationAlgorithmLevenberg trial decision (SURVEY.md §8a A13) + optimize() loop control.
-__global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
-    TRIAL_GUARD
-    __shared__ double sh[kBlock / 64];
-    double a = 0.0, b = 0.0;
-    if (!d.sharded) {
-        for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) a += d.part_lm[i];
-        for (int i = threadIdx.x; i < d.n_lms_blocks; i += kBlock) b += d.part_lms[i];
-    }
-    for (int i = threadIdx.x; i < d.n_ps; i += kBlock) b += d.part_ps[i];  // poses: replicated
-    double tempChi0 = block_sum<kBlock>(a, sh);
-    double scale0 = block_sum<kBlock>(b, sh);
-    if (d.sharded) {  // landmark terms summed over ranks
-        tempChi0 = d.red_dec[0];
-        scale0 += d.red_dec[1];
-    }
-    if (threadIdx.x != 0) return;
-    Ctrl *c = d.ctrl;
-    c->steps += 1;
-    double tempChi = tempChi0;
-    if (!c->solve_ok) tempChi = 1.7976931348623157e308;
-    const double scale = scale0 + 1e-3;
-    const double rho = (c->currentChi - tempChi) / scale;
-    c->tempChi = tempChi;
-    c->scale = scale;
-    c->rho = rho;
-    if (rho > 0 && isfinite(tempChi)) {
-        double alpha = 1. - pow((2 * rho - 1), 3);
-        alpha = fmin(alpha, 2. / 3.);
-        const double sf = fmax(1. / 3., alpha);
-        c->lambda *= sf;
-        c->ni = 2;
-        c->currentChi = tempChi;
-        c->accept = 1;
-        c->qmax += 1;
-    } else {
-        c->lambda *= c->ni;
-        c->ni *= 2;
-        c->accept = 0;
-        if (!isfinite(c->lambda)) c->broke = 1;
-        else c->qmax += 1;
-    }
-    if (c->accept) c->cur ^= 1;  // the trial becomes the current estimate
-    const bool again = !c->broke && rho < 0 && c->qmax < c->max_trials;
-    if (again) return;  // another damped trial of this iteration
-    // end of OptimizationAlgorithmLevenberg::solve(iter)
-    const int terminate = (c->qmax == c->max_trials || rho == 0 || !isfinite(c->lambda)) ? 1 : 0;
-    if (c->ntrace < kTraceCap)
-        d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, c->qmax, terminate, c->chi2_start, c->currentChi,
-                                               c->lambda_start, c->lambda};
-    c->iters_done[c->stage] += 1;
-    c->iter += 1;
-    if (terminate || c->iter >= c->max_iters[c->stage]) {  // optimize() returns
-        c->chi2_final[c->stage] = c->currentChi;
-        if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
-        else c->all_done = 1;
-    } else {
-        c->need_iter = 1;
     }
 }
 
