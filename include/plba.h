@@ -144,6 +144,60 @@ int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap);
 int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,
                       int32_t cap, int32_t *n);
 
+/* ---- Hand-rolled Levenberg–Marquardt local BA:
+ *   int MapHandler::levMarquardtOptimizationLBAForPluker(X_aux, kf_list, pt_list, ls_list,
+ *                                                         pt_obs_list, ls_obs_list)
+ *   (src/mapHandler.cpp:1618-2332; window lists built by localBundleAdjustmentForPluker, :1505-1615)
+ * One scalar residual r = ‖e‖ per observation with a Cauchy weight w = 1/(1+r²)
+ * (src2/auxiliar.cpp:556-559), H += w·JᵀJ, g += w·J·r, Marquardt damping H(i,i) += λ·H(i,i),
+ * DX = H⁻¹g, poses X_i ← log(exp(X_i)·exp(DX_i)⁻¹), points X += DX, lines updateOrthCoord.
+ * The window is the plba_graph of plba_upload, read as the reference's lists:
+ *   kf_fixed[k] == 0  <=>  KF k is in kf_list (local && kf_idx != 0, :1516)
+ *   kf_Tcw  = inverse_se3(T_kf_w), the MAP pose (:1657-1659): fixed KFs and every line
+ *             observation use it on every iteration (:2010-2012), free KFs on the first one
+ *   pt_xyz  = point3D (:1536), ln_orth = orthNDw = changePlukerToOrth(NDw) (:1577)
+ *   edges   = pt_obs_list / ls_obs_list (obs_list[i] / NDw_obs_list[i]); the info, Huber and
+ *             level fields are not used by this solver. */
+typedef struct plba_hlm_state {
+    const double *kf_x;        /* [n_kf][6] KeyFrame::x_kf_w = X_aux pose blocks [t; ω] (:1518)   */
+    const double *ln_pluker;   /* [n_ln][6] MapLine::NDw of the map (first linearisation, :1744)  */
+} plba_hlm_state;
+
+typedef struct plba_hlm_params {
+    double  lambda0;           /* SlamConfig::lambdaLbaLM()  1e-5 (src/slamConfig.cpp:65)         */
+    double  lambda_k;          /* SlamConfig::lambdaLbaK()   10   (src/slamConfig.cpp:66)         */
+    double  homog_th;          /* Config::homogTh()          1e-7 (src2/config.cpp:80)            */
+    double  min_error;         /* Config::minError()         1e-7 (src2/config.cpp:84)            */
+    double  min_error_change;  /* Config::minErrorChange()   1e-7 (src2/config.cpp:85)            */
+    int32_t max_iters;         /* SlamConfig::maxItersLba()  15   (src/slamConfig.cpp:67)         */
+    int32_t err_per_obs;       /* 0 = the reference: err /= (Npt_obs + Nls_obs), both counters stay
+                                  0 (:1642,1731,1849) so err becomes +inf and every step after the
+                                  first is accepted; 1 = divide by the observation count instead */
+} plba_hlm_params;
+
+typedef struct plba_hlm_result {
+    double  *kf_x;             /* [n_kf][6] X pose blocks at exit (KFs not in kf_list: input x)   */
+    double  *kf_Tcw;           /* [n_kf][12] inverse_se3(expmap_se3(x)) of each free KF, map pose
+                                  of the others                                                   */
+    double  *pt_xyz;           /* [n_pt][3]                                                       */
+    double  *ln_orth;          /* [n_ln][4]                                                       */
+    int32_t  linearizations;   /* H/g builds executed (1 .. max_iters)                            */
+    int32_t  solves;           /* SimplicialLDLT solves executed                                  */
+    int32_t  accepted;         /* solves whose DX was applied                                     */
+    int32_t  pad;
+    double   err;              /* last err (after the division)                                   */
+    double   lambda;           /* λ at exit                                                       */
+    double   dx_norm;          /* ‖DX‖ of the last solve                                          */
+    double   solve_ms;         /* wall time of the loop                                           */
+} plba_hlm_result;
+
+void plba_hlm_default_params(plba_hlm_params *p);
+/* The whole loop on the uploaded window, on the device (one captured step per iteration).
+ * Per-iteration records (plba_get_trace): stage 0, iter, trials 1, result 0 = DX applied,
+ * 1 = DX rejected (err > err_prev), 3 = stopped before the solve; chi2_start = chi2_end = err,
+ * lambda_start / lambda_end around the iteration. */
+int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params *p, plba_hlm_result *res);
+
 /* ---- Sharded windows: one context per GPU, one window split over nranks.
  * Landmarks (with all their edges) are partitioned by the keyframe range of their first
  * observation (kf_obs_list[0], the base KF of map_points_kf_idx); poses are replicated.

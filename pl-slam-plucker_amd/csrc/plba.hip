@@ -691,6 +691,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.X_init, X);
     UPLOAD(d.Xb[0], X);
     ALLOC(d.Xb[1], X.size());
+    ALLOC(d.xk[0], (size_t)n_kf * 6);
+    ALLOC(d.xk[1], (size_t)n_kf * 6);
     ALLOC(d.Lpb[0], (size_t)std::max(n_ln, 1) * 8);
     ALLOC(d.Lpb[1], (size_t)std::max(n_ln, 1) * 8);
     UPLOAD(d.kf_hidx, kf_hidx);
@@ -954,7 +956,8 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     Dev &d = ctx->d;
     *ctx->h_ctrl = init;
     PLBA_CHECK(hipMemcpyAsync(d.ctrl, ctx->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, ctx->stream));
-    if (d.n_ln > 0) {  // Plücker vectors of the current line states (read by k_linearize)
+    if (d.n_ln > 0 && !init.hlm) {  // Plücker vectors of the current line states (read by k_linearize;
+                                     // the hand-rolled LM starts from the map's NDw, uploaded instead)
         hipLaunchKernelGGL(k_line_pluker, dim3(blocks_for(d.n_ln)), dim3(kBlock), 0, ctx->stream, d);
         PLBA_CHECK(hipGetLastError());
     }
@@ -1337,6 +1340,81 @@ int plba_lba_plucker(plba_ctx *ctx, plba_result *res) {
         }
     }
     return PLBA_OK;
+}
+
+void plba_hlm_default_params(plba_hlm_params *p) {
+    if (!p) return;
+    p->lambda0 = 1e-5;          // src/slamConfig.cpp:65
+    p->lambda_k = 10.0;         // :66
+    p->homog_th = 1e-7;         // src2/config.cpp:80
+    p->min_error = 1e-7;        // :84
+    p->min_error_change = 1e-7; // :85
+    p->max_iters = 15;          // src/slamConfig.cpp:67
+    p->err_per_obs = 0;
+}
+
+// MapHandler::levMarquardtOptimizationLBAForPluker (src/mapHandler.cpp:1618-2332) on the uploaded
+// window: the captured step graph with the Ctrl::hlm variants of each kernel, one step per
+// iteration (linearise -> [stop] -> Schur solve -> decide), no host round trip inside a batch.
+int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params *p, plba_hlm_result *res) {
+    if (!ctx || !st || (ctx->n_kf && !st->kf_x) || (ctx->n_ln && !st->ln_pluker)) return PLBA_E_INVALID;
+    if (!ctx->uploaded) return PLBA_E_STATE;
+    (void)hipSetDevice(ctx->opts.device);
+    plba_hlm_params prm;
+    if (p) prm = *p;
+    else plba_hlm_default_params(&prm);
+    if (prm.max_iters < 1) {
+        ctx->set_error("max_iters must be >= 1");
+        return PLBA_E_INVALID;
+    }
+    int rc = plba_reset_estimates(ctx);
+    if (rc) return rc;
+    Dev &d = ctx->d;
+    ctx->trace.clear();
+    // X_aux pose blocks and the map's NDw (in this rank's device landmark order)
+    std::vector<double> Lm((size_t)std::max(d.n_ln, 1) * 8, 0.0);
+    for (int i = 0; i < d.n_ln; ++i) {
+        const int gl = ctx->lm_gpos[d.n_pt + i] - ctx->n_pt;
+        for (int k = 0; k < 6; ++k) Lm[(size_t)i * 8 + k] = st->ln_pluker[(size_t)gl * 6 + k];
+    }
+    if (d.n_kf) PLBA_CHECK(hipMemcpyAsync(d.xk[0], st->kf_x, sizeof(double) * (size_t)d.n_kf * 6, hipMemcpyHostToDevice, ctx->stream));
+    if (d.n_ln) PLBA_CHECK(hipMemcpyAsync(d.Lpb[0], Lm.data(), sizeof(double) * Lm.size(), hipMemcpyHostToDevice, ctx->stream));
+    auto t0 = std::chrono::steady_clock::now();
+    Ctrl c = schedule_init(ctx, 1);
+    c.max_iters[0] = prm.max_iters;
+    c.stage_robust[0] = 0;
+    c.stage_level[0] = 0;
+    c.hlm = 1;
+    c.hlm_lambda0 = prm.lambda0;
+    c.hlm_k = prm.lambda_k;
+    c.hlm_homog = prm.homog_th;
+    c.hlm_minerr = prm.min_error;
+    c.hlm_minchg = prm.min_error_change;
+    c.hlm_nobs = prm.err_per_obs ? (double)(ctx->Ep + ctx->El) : 0.0;
+    c.err_prev = 999999999.9;  // :1634
+    rc = run_schedule(ctx, c);
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    auto t1 = std::chrono::steady_clock::now();
+    if (rc) return rc;
+    if ((rc = collect_timing(ctx))) return rc;
+    ctx->robust = 1;
+    ctx->level = 0;
+    ctx->initialized = false;
+    if (!res) return PLBA_OK;
+    const Ctrl &h = *ctx->h_ctrl;
+    res->linearizations = h.hlm_lin;
+    res->solves = h.hlm_solves;
+    res->accepted = h.hlm_acc;
+    res->pad = 0;
+    res->err = h.currentChi;
+    res->lambda = h.lambda;
+    res->dx_norm = std::sqrt(h.dx2);
+    res->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (res->kf_x && d.n_kf) {
+        PLBA_CHECK(hipMemcpy(res->kf_x, d.xk[ctx->cur], sizeof(double) * (size_t)d.n_kf * 6, hipMemcpyDeviceToHost));
+        // KFs outside kf_list keep the caller's x (the device copy carries them through unchanged)
+    }
+    return plba_download(ctx, res->kf_Tcw, res->pt_xyz, res->ln_orth);
 }
 
 int plba_get_trace(plba_ctx *ctx, plba_iter_trace *out, int32_t cap, int32_t *n) {

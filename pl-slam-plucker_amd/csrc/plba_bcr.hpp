@@ -238,10 +238,15 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
                 ps[t] = v;
             }
             if (tid == 0) ps[BW * 24] = d.ctrl->lambda;
+            const bool hlm0 = d.ctrl->hlm != 0;
             for (int k = m + N * tid; k < d.n_kf; k += N * NT)
-                if (d.kf_hidx[k] < 0)
+                if (d.kf_hidx[k] < 0) {
 #pragma unroll
                     for (int q = 0; q < 12; ++q) Tt0[(size_t)k * 12 + q] = Tc0[(size_t)k * 12 + q];
+                    if (hlm0)
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) d.xk[cur0 ^ 1][(size_t)k * 6 + q] = d.xk[cur0][(size_t)k * 6 + q];
+                }
         }
         __syncthreads();
         BCR_STAMP(1);
@@ -507,9 +512,19 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
                 if (!failed)
 #pragma unroll
                     for (int q = 0; q < 6; ++q) d.xp[6 * h + q] = x[q];
+                if (d.ctrl->hlm) {  // hand-rolled LM: se(3) update, ‖DX‖² part
+                    const int kf = s_kf[tid];
+                    double xn[6];
 #pragma unroll
-                for (int q = 0; q < 6; ++q) sc += x[q] * (lam * x[q] + pp[12 + q]);
-                pose_oplus(pp, x, d.Tb[cur0 ^ 1] + (size_t)s_kf[tid] * 12);
+                    for (int q = 0; q < 6; ++q) sc += x[q] * x[q];
+                    hlm_pose_update(d.xk[cur0] + (size_t)kf * 6, x, xn, d.Tb[cur0 ^ 1] + (size_t)kf * 12);
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) d.xk[cur0 ^ 1][(size_t)kf * 6 + q] = xn[q];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) sc += x[q] * (lam * x[q] + pp[12 + q]);
+                    pose_oplus(pp, x, d.Tb[cur0 ^ 1] + (size_t)s_kf[tid] * 12);
+                }
             }
         }
         const double ssum = block_sum<NT>(sc, s_sum);

@@ -64,7 +64,14 @@ struct Ctrl {
     int32_t max_trials, ntrace, any_active, cur;      // cur: which state buffer is current
     int32_t steps;                                     // step graphs that did work (diagnostic)
     int32_t dev_error;                                 // a bounded in-kernel wait timed out
+    // hand-rolled LM (plba_hlm_lba, src/mapHandler.cpp:1618-2332): the same step graph with the
+    // scalar-residual linearisation, Marquardt damping, se(3) pose update and its own decision
+    int32_t hlm;                                       // 0: g2o Levenberg, 1: levMarquardtOptimizationLBAForPluker
+    int32_t hlm_lin, hlm_solves, hlm_acc;              // linearisations, solves, applied updates
     int32_t pad[2];
+    double hlm_lambda0, hlm_k, hlm_homog, hlm_minerr, hlm_minchg;
+    double hlm_nobs;                                   // err divisor (0 = the reference's Npt_obs+Nls_obs)
+    double err_prev, dx2;                              // err of the previous linearisation, ‖DX‖² of the last solve
 };
 
 // All device pointers of one window (passed by value to every kernel).
@@ -79,6 +86,7 @@ struct Dev {
     // flips ctrl->cur (g2o's push/pop/discardTop without a copy)
     double *Tb[2], *T_init;             // [n_kf][12]
     double *Xb[2], *X_init;             // [n_lm][4]
+    double *xk[2];                      // [n_kf][6] se(3) pose vectors X_i of the hand-rolled LM
     double *Lpb[2];                     // [n_ln][8]: Plücker vector (6) of each line at Xb[i]
                                         //   (k_line_pluker at schedule start, then k_lm_solve)
     int32_t *kf_hidx;                   // [n_kf]
@@ -295,7 +303,42 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
             }
             d.e_active[e] = d.e_level[e] == cc->stage_level[nxt] ? 1 : 0;
         }
-        if (d.e_active[e]) {
+        if (d.e_active[e] && cc->hlm) {
+            // hand-rolled LM (src/mapHandler.cpp:1909-2103): one scalar residual r = ‖e‖ with
+            // Cauchy weight w; row 0 of A/B holds √w·J, c = (√w·r, 0), so Σ AᵀA = Σ w JᵀJ and
+            // Σ Aᵀc = Σ w J r = g. Point observations read the current pose (the map pose of
+            // fixed KFs and, before the first update, of every KF); line observations always
+            // read the map pose T_init (:2010-2012) and the current NDw (the map's on the first
+            // linearisation, uploaded into Lpb by plba_hlm_lba).
+            const int lm = d.e_lm[e], kf = d.e_kf[e];
+            const double *obs = d.e_obs + (size_t)e * 4;
+            double r, w, Jp[6], Jl[4];
+            if (e < d.Ep) {
+                hlm_point(Tcur(d) + (size_t)kf * 12, Xcur(d) + (size_t)lm * 4, obs, d.cam, cc->hlm_homog, r, w, Jp, Jl);
+            } else {
+                const double *Lc = d.Lpb[cc->cur] + (size_t)(lm - d.n_pt) * 8;
+                double L[6];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) L[k] = Lc[k];
+                hlm_line(d.T_init + (size_t)kf * 12, L, obs, d.cam, cc->hlm_homog, r, w, Jp, Jl);
+            }
+            d.chi2_last[e] = r * r;
+            rc = r * r * w;
+            const double sw = sqrt(w);
+            const bool pose_free = d.e_hidx[e] >= 0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                A[k] = pose_free ? sw * Jp[k] : 0.0;
+                A[6 + k] = 0.0;
+            }
+            c[0] = sw * r;
+            c[1] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                B[k] = sw * Jl[k];
+                B[4 + k] = 0.0;
+            }
+        } else if (d.e_active[e]) {
             const int lm = d.e_lm[e], kf = d.e_kf[e];
             const double *T = Tcur(d) + (size_t)kf * 12;
             const double *X = Xcur(d) + (size_t)lm * 4;
@@ -557,6 +600,28 @@ __global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
                 return;
             }
         }
+        if (c->hlm) {  // src/mapHandler.cpp:1849-1858 (first linearisation), :2108-2112 (later)
+            const double err = chi / c->hlm_nobs;  // reference: / (Npt_obs + Nls_obs) == / 0
+            c->hlm_lin += 1;
+            if (c->iter == 0) {
+                c->maxdiag = mx;
+                c->lambda = c->hlm_lambda0 * mx;
+            } else if (fabs(err - c->err_prev) < c->hlm_minchg || err < c->hlm_minerr) {
+                if (c->ntrace < kTraceCap)
+                    d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, 0, 3, err, err, c->lambda, c->lambda};
+                c->currentChi = err;
+                c->chi2_final[c->stage] = err;
+                c->need_iter = 0;
+                c->all_done = 1;
+                return;
+            }
+            c->currentChi = err;
+            c->chi2_start = err;
+            c->lambda_start = c->lambda;
+            c->accept = 0;
+            c->need_iter = 0;
+            return;
+        }
         c->currentChi = chi;
         c->chi2_start = chi;
         if (c->iter == 0) {  // computeLambdaInit: τ·max|H_jj|, ν = 2
@@ -593,7 +658,11 @@ __device__ __forceinline__ void rcs_finalize_entry(const Dev &d, int b, int e, d
         // a free pose with no active edge is not in g2o's system (SparseOptimizer activation,
         // SURVEY.md §8 A13); its all-zero block row becomes I (x = 0 exactly) instead of λI,
         // which would be a zero pivot at λ = 0
-        if (r == c) h += d.pact[i1] != 0.0 ? d.ctrl->lambda : 1.0;
+        // (hand-rolled LM: Marquardt damping H(i,i) += λ·H(i,i), src/mapHandler.cpp:2114-2115)
+        if (r == c) {
+            const Ctrl *cg = d.ctrl;
+            h += d.pact[i1] == 0.0 ? 1.0 : cg->hlm ? cg->lambda * d.Hpp[(size_t)i1 * 36 + e] : cg->lambda;
+        }
         if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
         else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
         if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1)) * 36 + e] = h;
@@ -721,6 +790,7 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
     __shared__ double sh_pu[NT / 64];
     double sc = 0.0;
     const double lam = d.ctrl->lambda;
+    const int hlm = d.ctrl->hlm, cur = d.ctrl->cur;
     const double *Tc0 = Tcur(d);
     double *Tt0 = Ttrial(d);
     for (int k = threadIdx.x; k < d.n_kf; k += NT) {
@@ -729,7 +799,17 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
         const int h = d.kf_hidx[k];
         // a free pose with no active edge has a zero RCS row: x = 0 exactly and the oplus is an
         // exact identity, so every free pose is updated
-        if (h >= 0) {
+        if (h >= 0 && hlm) {  // X_i <- log(exp(X_i)·exp(DX_i)⁻¹); sc = ‖DX‖² part
+            double x[6], xn[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                x[i] = d.xp[6 * h + i];
+                sc += x[i] * x[i];
+            }
+            hlm_pose_update(d.xk[cur] + (size_t)k * 6, x, xn, Tt);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) d.xk[cur ^ 1][(size_t)k * 6 + i] = xn[i];
+        } else if (h >= 0) {
             double x[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
@@ -740,6 +820,9 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
         } else {
 #pragma unroll
             for (int i = 0; i < 12; ++i) Tt[i] = Tc[i];
+            if (hlm)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) d.xk[cur ^ 1][(size_t)k * 6 + i] = d.xk[cur][(size_t)k * 6 + i];
         }
     }
     const double s = block_sum<NT>(sc, sh_pu);
@@ -1529,7 +1612,7 @@ __global__ __launch_bounds__(kBlock) void k_pose_update(Dev d) {
 // ---------------------------------------------------------------- edge-parallel trial path
 // per landmark: (Hll + λI) = L Lᵀ, g = L⁻¹ b_l (packed lower; recomputed where needed — 4x4,
 // cheaper than a kernel boundary)
-__device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, double (&L)[10], double (&g)[4]) {
+__device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, bool mul, double (&L)[10], double (&g)[4]) {
     const int DIM = is_point_lm(d, l) ? 3 : 4;
     double H[10];
 #pragma unroll
@@ -1539,7 +1622,7 @@ __device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, double 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         if (j < DIM) {
-            double sj = H[pk(j, j)] + lam;
+            double sj = H[pk(j, j)] + (mul ? lam * H[pk(j, j)] : lam);
 #pragma unroll
             for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
             const double djj = sqrt(sj);
@@ -1573,7 +1656,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
     const int l = d.e_lm[e];
     const int DIM = e < d.Ep ? 3 : 4;
     double L[10], g[4], B[8];
-    lm_chol(d, l, d.ctrl->lambda, L, g);
+    lm_chol(d, l, d.ctrl->lambda, d.ctrl->hlm != 0, L, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) B[k] = d.B[(size_t)e * 8 + k];
     double z[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -1759,6 +1842,43 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
     if (threadIdx.x != 0) return;
     Ctrl *c = d.ctrl;
     c->steps += 1;
+    if (c->hlm) {  // src/mapHandler.cpp:1867-1895 (first step), :2121-2156
+        const double lam0 = c->lambda;
+        const bool first = c->iter == 0;
+        int result = 0;
+        c->hlm_solves += 1;
+        c->dx2 = scale0;
+        bool apply;
+        if (first) {
+            apply = true;
+        } else if (c->currentChi > c->err_prev) {
+            c->lambda /= c->hlm_k;
+            apply = false;
+            result = 1;
+        } else {
+            c->lambda *= c->hlm_k;
+            apply = true;
+        }
+        apply = apply && c->solve_ok;  // (an LDLᵀ breakdown leaves X unchanged)
+        if (apply) {
+            c->cur ^= 1;
+            c->hlm_acc += 1;
+        }
+        if (c->ntrace < kTraceCap)
+            d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, 1, result, c->currentChi, c->currentChi, lam0,
+                                                   c->lambda};
+        c->iters_done[c->stage] += 1;
+        c->iter += 1;
+        const bool small = !first && sqrt(scale0) < c->hlm_minchg;
+        c->err_prev = c->currentChi;
+        if (small || c->iter >= c->max_iters[c->stage]) {
+            c->chi2_final[c->stage] = c->currentChi;
+            c->all_done = 1;
+        } else {
+            c->need_iter = 1;
+        }
+        return;
+    }
     double tempChi = tempChi0;
     if (!c->solve_ok) tempChi = 1.7976931348623157e308;
     const double scale = scale0 + 1e-3;
@@ -1818,6 +1938,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
     const bool robust = cg->robust != 0;
     const double lam = cg->lambda;
     const int cur = cg->cur;
+    const bool hlm = cg->hlm != 0;
     // ---- round 1: landmark record + this lane's edge slots
     const bool act = live && d.lm_active[lc] != 0;
     const int off0 = d.lm_off[lc], off1 = d.lm_off[lc + 1];
@@ -1878,7 +1999,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (j < DIM) {
-                        double sj = H[pk(j, j)] + lam;
+                        double sj = H[pk(j, j)] + (hlm ? lam * H[pk(j, j)] : lam);
 #pragma unroll
                         for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
                         const double djj = sqrt(sj);
@@ -1923,7 +2044,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
             if (q == 0) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    if (i < DIM) sc += x[i] * (lam * x[i] + bl[i]);
+                    if (i < DIM) sc += hlm ? x[i] * x[i] : x[i] * (lam * x[i] + bl[i]);
             }
             double X[4] = {0, 0, 0, 0}, Lp[6] = {0, 0, 0, 0, 0, 0};
             if (pt) {
@@ -1943,11 +2064,11 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
             // the landmark's edges at the trial state (computeActiveErrors of the trial); the
             // trial poses were written by the factorisation kernel
             const double delta = pt ? d.huber_pt : d.huber_ln;
-            if (!(d.diag & 2))
+            if (!(d.diag & 2) && !hlm)  // (the hand-rolled LM scores a step at the next linearisation)
 #pragma unroll
             for (int j = 0; j < kLmSlots; ++j)
                 if (sv[j] && sl[j].act) chi += lm_eval(d, sl[j], Ts[j], pt, X, Lp, robust, delta);
-            for (int e = off0 + q + kLmLanes * kLmSlots; e < off1; e += kLmLanes) {  // long tracks
+            for (int e = off0 + q + kLmLanes * kLmSlots; e < off1 && !hlm; e += kLmLanes) {  // long tracks
                 if (!d.e_active[e]) continue;
                 LmEdge s;
                 lm_load_edge(d, e, s);

@@ -269,4 +269,237 @@ PLBA_HD void line_jac(const double *T, const double *orth, const double *L, cons
     }
 }
 
+// ================= hand-rolled LM (MapHandler::levMarquardtOptimizationLBAForPluker) =========
+// se(3) maps of src2/auxiliar.cpp:113-173 on row-major 4x4 (x = [t; ω]). No FMA contraction:
+// logmap_se3 divides by sin θ, so near θ = π a fused multiply-add in 1 − cos²θ or in R = I + s·sinθ
+// + s²(1 − cosθ) moves X_i by ~1e-10 per step relative to the unfused reference arithmetic.
+// unfused 3x3 helpers for the se(3) maps below (an inlined callee keeps its own contraction
+// setting, so mat3mul / mat3vec would still fuse inside a contract(off) caller)
+PLBA_HD void m3mul_nc(const double *A, const double *B, double *C) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[i * 3 + j] = A[i * 3 + 0] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
+}
+PLBA_HD void m3vec_nc(const double *R, const double *v, double *r) {
+#pragma clang fp contract(off)
+    r[0] = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    r[1] = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    r[2] = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+}
+PLBA_HD void se3_exp(const double *x, double *T) {  // expmap_se3 (:124-141)
+#pragma clang fp contract(off)
+    const double w0 = x[3], w1 = x[4], w2 = x[5];
+    double t0 = x[0], t1 = x[1], t2 = x[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (!(theta < 0.000001)) {
+        const double w[3] = {w0, w1, w2};
+        double s[9], ss[9];
+        vechat(w, s);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) s[i] /= theta;
+        m3mul_nc(s, s, ss);
+        const double st = sin(theta), ct = 1.0 - cos(theta);
+        double V[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double I = (i % 4 == 0) ? 1.0 : 0.0;
+            R[i] = (I + s[i] * st) + ss[i] * ct;
+            V[i] = (I + s[i] * ct / theta) + ss[i] * (theta - st) / theta;
+        }
+        const double tv[3] = {t0, t1, t2};
+        double r[3];
+        m3vec_nc(V, tv, r);
+        t0 = r[0]; t1 = r[1]; t2 = r[2];
+    }
+    T[0] = R[0]; T[1] = R[1]; T[2] = R[2];  T[3] = t0;
+    T[4] = R[3]; T[5] = R[4]; T[6] = R[5];  T[7] = t1;
+    T[8] = R[6]; T[9] = R[7]; T[10] = R[8]; T[11] = t2;
+    T[12] = 0; T[13] = 0; T[14] = 0; T[15] = 1;
+}
+PLBA_HD void inv3_cof(const double *m, double *r) {  // Eigen's closed-form 3x3 inverse
+#pragma clang fp contract(off)
+    const double c0 = m[4] * m[8] - m[5] * m[7];
+    const double c1 = m[5] * m[6] - m[3] * m[8];
+    const double c2 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c0 + m[1] * c1 + m[2] * c2;
+    r[0] = c0 / det; r[3] = c1 / det; r[6] = c2 / det;
+    r[1] = (m[2] * m[7] - m[1] * m[8]) / det;
+    r[4] = (m[0] * m[8] - m[2] * m[6]) / det;
+    r[7] = (m[1] * m[6] - m[0] * m[7]) / det;
+    r[2] = (m[1] * m[5] - m[2] * m[4]) / det;
+    r[5] = (m[2] * m[3] - m[0] * m[5]) / det;
+    r[8] = (m[0] * m[4] - m[1] * m[3]) / det;
+}
+PLBA_HD void se3_log(const double *T, double *x) {  // logmap_se3 (:143-173)
+#pragma clang fp contract(off)
+    const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+    const double Vt[3] = {T[3], T[7], T[11]};
+    double w[3] = {0, 0, 0};
+    double V[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double cosine = (R[0] + R[4] + R[8] - 1.0) / 2.0;
+    if (cosine > 1.0) cosine = 1.0;
+    else if (cosine < -1.0) cosine = -1.0;
+    double sine = sqrt(1.0 - cosine * cosine);
+    if (sine > 1.0) sine = 1.0;
+    else if (sine < -1.0) sine = -1.0;
+    const double theta = acos(cosine);
+    if (theta > 0.000001) {
+        w[0] = theta * (R[7] - R[5]) / (2.0 * sine);
+        w[1] = theta * (R[2] - R[6]) / (2.0 * sine);
+        w[2] = theta * (R[3] - R[1]) / (2.0 * sine);
+        double s[9], ss[9];
+        vechat(w, s);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) s[i] /= theta;
+        m3mul_nc(s, s, ss);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double I = (i % 4 == 0) ? 1.0 : 0.0;
+            V[i] = (I + s[i] * (1.0 - cosine) / theta) + ss[i] * (theta - sine) / theta;
+        }
+    }
+    double Vi[9], t[3];
+    inv3_cof(V, Vi);
+    m3vec_nc(Vi, Vt, t);
+    x[0] = t[0]; x[1] = t[1]; x[2] = t[2];
+    x[3] = w[0]; x[4] = w[1]; x[5] = w[2];
+}
+// inverse_se3 (:113-122) of a row-major 4x4 into a row-major 3x4 [Rᵀ | −Rᵀt]
+PLBA_HD void se3_inv34(const double *T, double *Ti) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Ti[i * 4 + j] = T[j * 4 + i];
+        Ti[i * 4 + 3] = -(T[0 * 4 + i] * T[3] + T[1 * 4 + i] * T[7] + T[2 * 4 + i] * T[11]);
+    }
+}
+// X_i <- logmap_se3(expmap_se3(X_i) · inverse_se3(expmap_se3(DX_i)))  (src/mapHandler.cpp:1868-1873),
+// and the Tiw = inverse_se3(expmap_se3(X_i)) the next linearisation reads (:1922-1927)
+PLBA_HD void hlm_pose_update(const double *x, const double *dx, double *xn, double *Tcw) {
+#pragma clang fp contract(off)
+    double Tp[16], E[16], Ei[12], Tc[16];
+    se3_exp(x, Tp);
+    se3_exp(dx, E);
+    se3_inv34(E, Ei);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double s = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s += Tp[i * 4 + k] * Ei[k * 4 + j];
+            s += Tp[i * 4 + 3] * (j == 3 ? 1.0 : 0.0);
+            Tc[i * 4 + j] = s;
+        }
+    se3_log(Tc, xn);
+    double Tn[16];
+    se3_exp(xn, Tn);
+    se3_inv34(Tn, Tcw);
+}
+
+// One point observation as the hand-rolled LM forms it (src/mapHandler.cpp:1655-1698): r = ‖e‖,
+// Cauchy weight w (src2/auxiliar.cpp:556-559), the pose row Jp and the landmark row Jl.
+PLBA_HD void hlm_point(const double *T, const double *X, const double *obs, const Cam &c, double hth, double &r,
+                       double &w, double *Jp, double *Jl) {
+    double P[3];
+    point_pc(T, X, P);
+    const double u = c.cx + c.fx * P[0] / P[2], v = c.cy + c.fy * P[1] / P[2];  // cam->projection
+    const double dx = obs[0] - u, dy = obs[1] - v;
+    r = sqrt(dx * dx + dy * dy);
+    const double gx = P[0], gy = P[1], gz = P[2];
+    const double gz2 = 1.0 / fmax(hth, gz * gz);
+    const double fxdx = c.fx * dx, fydy = c.fy * dy;
+    const double m = fmax(hth, r);
+    Jp[0] = (gz2 * fxdx * gz) / m;
+    Jp[1] = (gz2 * fydy * gz) / m;
+    Jp[2] = (-gz2 * (fxdx * gx + fydy * gy)) / m;
+    Jp[3] = (-gz2 * (fxdx * gx * gy + fydy * gy * gy + fydy * gz * gz)) / m;
+    Jp[4] = (gz2 * (fxdx * gx * gx + fxdx * gz * gz + fydy * gx * gy)) / m;
+    Jp[5] = (gz2 * (fydy * gx * gz - fxdx * gy * gz)) / m;
+    const double j0 = gz2 * fxdx * gz, j1 = gz2 * fydy * gz, j2 = -gz2 * (fxdx * gx + fydy * gy);
+    Jl[0] = (j0 * T[0] + j1 * T[4] + j2 * T[8]) / m;  // Jᵀ · R
+    Jl[1] = (j0 * T[1] + j1 * T[5] + j2 * T[9]) / m;
+    Jl[2] = (j0 * T[2] + j1 * T[6] + j2 * T[10]) / m;
+    Jl[3] = 0.0;
+    w = 1.0 / (1.0 + r * r);
+}
+
+// One line observation (src/mapHandler.cpp:1744-1811): NDc = TransformForPluker(Tiw, NDw),
+// l = plukerK·NDc.head(3), the pose row from fai_e·[K 0]·fai_lineCurr_RT and the landmark row
+// from fai_e·[K 0]·getTransformMatrixForPluker(Tiw)·jacobianFromPlukerToOrth(Rw, Ww)
+// (src/mapFeatures.cpp:251-266), both combined as (jac0·e0 + jac1·e1)/max(homogTh, r).
+PLBA_HD void hlm_line(const double *T, const double *L, const double *obs, const Cam &c, double hth, double &r,
+                      double &w, double *Jp, double *Jl) {
+    const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+    const double t[3] = {T[3], T[7], T[11]};
+    const double nn = sqrt(L[0] * L[0] + L[1] * L[1] + L[2] * L[2]);
+    const double dn = sqrt(L[3] * L[3] + L[4] * L[4] + L[5] * L[5]);
+    const double cr[3] = {L[1] * L[5] - L[2] * L[4], L[2] * L[3] - L[0] * L[5], L[0] * L[4] - L[1] * L[3]};
+    const double cn = sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+    const double fw = sqrt(nn * nn + dn * dn), w1 = nn / fw, w2 = dn / fw;
+    double u1[3], u2[3], u3[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        u1[i] = L[i] / nn;
+        u2[i] = L[3 + i] / dn;
+        u3[i] = cr[i] / cn;
+    }
+    double St[9], StR[9], Rn[3], Rd[3], tRd[3];
+    vechat(t, St);
+    mat3mul(St, R, StR);
+    mat3vec(R, L, Rn);
+    mat3vec(R, L + 3, Rd);
+    mat3vec(StR, L + 3, tRd);
+    const double nc[3] = {Rn[0] + tRd[0], Rn[1] + tRd[1], Rn[2] + tRd[2]};
+    const double K[9] = {c.fy, 0, 0, 0, c.fx, 0, -c.fy * c.cx, -c.fx * c.cy, c.fx * c.fy};
+    double l[3];
+    mat3vec(K, nc, l);
+    const double lx = l[0], ly = l[1], lz = l[2];
+    const double fenmu = sqrt(lx * lx + ly * ly);
+    const double e[2] = {(obs[0] * lx + obs[1] * ly + lz) / fenmu, (obs[2] * lx + obs[3] * ly + lz) / fenmu};
+    r = sqrt(e[0] * e[0] + e[1] * e[1]);
+    double SRd[9], SRn[9], StSRd[9];
+    vechat(Rd, SRd);
+    vechat(Rn, SRn);
+    mat3mul(St, SRd, StSRd);
+    double jp[2][6], jl[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double a = obs[2 * k], b = obs[2 * k + 1];
+        const double fe[3] = {a * fenmu - lx * e[k] * fenmu * fenmu, b * fenmu - ly * e[k] * fenmu * fenmu, fenmu};
+        double v[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[j] = fe[0] * K[j] + fe[1] * K[3 + j] + fe[2] * K[6 + j];
+        double q[6];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            jp[k][j] = v[0] * (-SRd[j]) + v[1] * (-SRd[3 + j]) + v[2] * (-SRd[6 + j]);
+            jp[k][3 + j] = v[0] * (-SRn[j] - StSRd[j]) + v[1] * (-SRn[3 + j] - StSRd[3 + j]) +
+                           v[2] * (-SRn[6 + j] - StSRd[6 + j]);
+            q[j] = v[0] * R[j] + v[1] * R[3 + j] + v[2] * R[6 + j];
+            q[3 + j] = v[0] * StR[j] + v[1] * StR[3 + j] + v[2] * StR[6 + j];
+        }
+        // q · jacobianFromPlukerToOrth (rows 0-2: n part, rows 3-5: d part)
+        double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            s0 += q[3 + i] * (w2 * u3[i]);
+            s1 += q[i] * (-w1 * u3[i]);
+            s2 += q[i] * (-w1 * u2[i]) + q[3 + i] * (-w2 * u1[i]);
+            s3 += q[i] * (-w2 * u1[i]) + q[3 + i] * (w1 * u2[i]);
+        }
+        jl[k][0] = s0; jl[k][1] = s1; jl[k][2] = s2; jl[k][3] = s3;
+    }
+    const double m = fmax(hth, r);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) Jp[j] = (jp[0][j] * e[0] + jp[1][j] * e[1]) / m;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Jl[j] = (jl[0][j] * e[0] + jl[1][j] * e[1]) / m;
+    w = 1.0 / (1.0 + r * r);
+}
+
 }  // namespace plba

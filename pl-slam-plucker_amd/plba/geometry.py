@@ -120,3 +120,57 @@ def transform_pluker(Tcw: np.ndarray, L: np.ndarray) -> np.ndarray:
     nc = (R @ n[..., None])[..., 0] + (skew(t) @ R @ d[..., None])[..., 0]
     dc = (R @ d[..., None])[..., 0]
     return np.concatenate([nc, dc], -1)
+
+
+def expmap_se3(x: np.ndarray) -> np.ndarray:
+    """``expmap_se3`` (src2/auxiliar.cpp:124-141), batched (...,6) [t; ω] -> (...,4,4)."""
+    x = np.asarray(x, dtype=np.float64)
+    w = x[..., 3:]
+    t = x[..., :3]
+    th = np.linalg.norm(w, axis=-1)[..., None, None]
+    small = th < 0.000001
+    ths = np.where(small, 1.0, th)
+    s = skew(w) / ths
+    ss = s @ s
+    eye = np.broadcast_to(np.eye(3), s.shape)
+    R = np.where(small, eye, eye + s * np.sin(ths) + ss * (1.0 - np.cos(ths)))
+    V = eye + s * (1.0 - np.cos(ths)) / ths + ss * (ths - np.sin(ths)) / ths
+    tt = np.where(small[..., 0], t, (V @ t[..., None])[..., 0])
+    T = np.zeros(x.shape[:-1] + (4, 4))
+    T[..., :3, :3] = R
+    T[..., :3, 3] = tt
+    T[..., 3, 3] = 1.0
+    return T
+
+
+def logmap_se3(T: np.ndarray) -> np.ndarray:
+    """``logmap_se3`` (src2/auxiliar.cpp:143-173), batched (...,4,4) -> (...,6) [t; ω]."""
+    T = np.asarray(T, dtype=np.float64)
+    R = T[..., :3, :3]
+    Vt = T[..., :3, 3]
+    cosine = np.clip((np.trace(R, axis1=-2, axis2=-1) - 1.0) / 2.0, -1.0, 1.0)
+    sine = np.clip(np.sqrt(1.0 - cosine * cosine), -1.0, 1.0)
+    theta = np.arccos(cosine)
+    big = theta > 0.000001
+    ths = np.where(big, theta, 1.0)
+    sn = np.where(big, sine, 1.0)
+    w_hat = ths[..., None, None] * (R - np.swapaxes(R, -1, -2)) / (2.0 * sn[..., None, None])
+    w = np.stack([w_hat[..., 2, 1], w_hat[..., 0, 2], w_hat[..., 1, 0]], -1)
+    w = np.where(big[..., None], w, 0.0)
+    s = skew(w) / ths[..., None, None]
+    eye = np.broadcast_to(np.eye(3), R.shape)
+    V = eye + s * ((1.0 - cosine) / ths)[..., None, None] + (s @ s) * ((ths - sine) / ths)[..., None, None]
+    V = np.where(big[..., None, None], V, eye)
+    t = (np.linalg.inv(V) @ Vt[..., None])[..., 0]
+    return np.concatenate([t, w], -1)
+
+
+def inverse_se3(T: np.ndarray) -> np.ndarray:
+    """``inverse_se3`` (src2/auxiliar.cpp:113-122), batched (...,4,4) -> (...,4,4)."""
+    T = np.asarray(T, dtype=np.float64)
+    out = np.zeros_like(T)
+    Rt = np.swapaxes(T[..., :3, :3], -1, -2)
+    out[..., :3, :3] = Rt
+    out[..., :3, 3] = -(Rt @ T[..., :3, 3][..., None])[..., 0]
+    out[..., 3, 3] = 1.0
+    return out

@@ -27,6 +27,7 @@ EXPORTED = [
     "plba_refresh_edge_errors", "plba_get_edge_chi2", "plba_download", "plba_lba_plucker", "plba_get_trace",
     "plba_synchronize", "plba_enable_kernel_timing", "plba_kernel_times", "plba_structure_stats",
     "plba_shard_plan", "plba_comm_unique_id", "plba_comm_init_rccl", "plba_comm_init_host",
+    "plba_hlm_default_params", "plba_hlm_lba",
 ]
 
 # int (*plba_host_allreduce_fn)(void *user, double *buf, int64_t n)
@@ -76,9 +77,13 @@ def load(path: Optional[str] = None):
     L.plba_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
     L.plba_comm_init_rccl.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
     L.plba_comm_init_host.argtypes = [vp, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, vp]
+    L.plba_hlm_default_params.argtypes = [C.POINTER(capi.PlbaHlmParams)]
+    L.plba_hlm_default_params.restype = None
+    L.plba_hlm_lba.argtypes = [vp, C.POINTER(capi.PlbaHlmState), C.POINTER(capi.PlbaHlmParams),
+                               C.POINTER(capi.PlbaHlmResult)]
     for name in EXPORTED:
         f = getattr(L, name)
-        if name not in ("plba_default_opts", "plba_last_error"):
+        if name not in ("plba_default_opts", "plba_last_error", "plba_hlm_default_params"):
             f.restype = C.c_int
     _lib = L
     return L
@@ -225,6 +230,23 @@ class Solver:
             self._check(self.L.plba_lba_plucker(self.ctx, C.byref(r)), "plba_lba_plucker")
             out = dict(iters=np.array([r.iters[0], r.iters[1]]), chi2=np.array([r.chi2[0], r.chi2[1]]),
                        solve_ms=r.solve_ms)
+        if with_trace:
+            out["trace"] = self.trace()
+        return out
+
+    def hlm_lba(self, win, params=None, with_trace: bool = True) -> dict:
+        """levMarquardtOptimizationLBAForPluker (src/mapHandler.cpp:1618-2332) on the uploaded window.
+
+        ``win`` is a plba.hlm.HlmWindow whose ``graph`` was uploaded with :meth:`upload`."""
+        g = self.graph
+        if params is None:
+            params = capi.PlbaHlmParams()
+            self.L.plba_hlm_default_params(C.byref(params))
+        sv = capi.HlmStateView(win.kf_x, win.ln_pluker)
+        rb = capi.HlmResultBuffers(g)
+        self._check(self.L.plba_hlm_lba(self.ctx, C.byref(sv.struct), C.byref(params), C.byref(rb.struct)),
+                    "plba_hlm_lba")
+        out = rb.as_dict()
         if with_trace:
             out["trace"] = self.trace()
         return out

@@ -131,3 +131,73 @@ def pluker_to_orth(L):
     o = np.zeros(4)
     lib().refcpu_pluker_to_orth(_p(L), _p(o))
     return o
+
+
+# ---- hand-rolled LM oracle (oracle/refhlm.cpp)
+class RefhlmOpts(C.Structure):
+    _fields_ = [("dense", C.c_int32), ("verbose", C.c_int32)]
+
+
+def _hlm_lib():
+    L = lib()
+    if not getattr(L, "_hlm_ready", False):
+        dp = C.POINTER(C.c_double)
+        L.refhlm_lba.argtypes = [C.POINTER(capi.PlbaGraph), C.POINTER(capi.PlbaHlmState), C.POINTER(capi.PlbaHlmParams),
+                                 C.POINTER(RefhlmOpts), C.POINTER(capi.PlbaHlmResult), C.POINTER(capi.PlbaIterTrace),
+                                 C.c_int32, C.POINTER(C.c_int32)]
+        L.refhlm_lba.restype = C.c_int
+        L.refhlm_point_obs.argtypes = [dp, dp, dp] + [C.c_double] * 5 + [dp, dp, dp, dp]
+        L.refhlm_line_obs.argtypes = [dp, dp, dp] + [C.c_double] * 5 + [dp, dp, dp, dp]
+        L.refhlm_expmap.argtypes = [dp, dp]
+        L.refhlm_logmap.argtypes = [dp, dp]
+        L.refhlm_inverse_se3.argtypes = [dp, dp]
+        L._hlm_ready = True
+    return L
+
+
+def hlm_lba(win, params=None, dense: bool = False) -> dict:
+    """levMarquardtOptimizationLBAForPluker on an HlmWindow (plba.hlm.hlm_window)."""
+    g = win.graph
+    gv = capi.GraphView(g)
+    sv = capi.HlmStateView(win.kf_x, win.ln_pluker)
+    rb = capi.HlmResultBuffers(g)
+    cap = 64
+    tr = (capi.PlbaIterTrace * cap)()
+    n = C.c_int32(0)
+    p = params if params is not None else capi.hlm_params()
+    o = RefhlmOpts(dense=int(dense), verbose=0)
+    rc = _hlm_lib().refhlm_lba(C.byref(gv.struct), C.byref(sv.struct), C.byref(p), C.byref(o), C.byref(rb.struct), tr,
+                               cap, C.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"refhlm_lba failed: {rc}")
+    out = rb.as_dict()
+    out["trace"] = capi.trace_to_array(tr, min(n.value, cap))
+    return out
+
+
+def hlm_point_obs(Tcw, xyz, obs, cam, homog_th=1e-7):
+    a = [np.ascontiguousarray(v, np.float64).reshape(-1) for v in (Tcw, xyz, obs)]
+    r, w, Jp, Jl = np.zeros(1), np.zeros(1), np.zeros(6), np.zeros(3)
+    _hlm_lib().refhlm_point_obs(*[_p(v) for v in a], *cam, homog_th, _p(r), _p(w), _p(Jp), _p(Jl))
+    return r[0], w[0], Jp, Jl
+
+
+def hlm_line_obs(Tcw, pluker, obs, cam, homog_th=1e-7):
+    a = [np.ascontiguousarray(v, np.float64).reshape(-1) for v in (Tcw, pluker, obs)]
+    r, w, Jp, Jl = np.zeros(1), np.zeros(1), np.zeros(6), np.zeros(4)
+    _hlm_lib().refhlm_line_obs(*[_p(v) for v in a], *cam, homog_th, _p(r), _p(w), _p(Jp), _p(Jl))
+    return r[0], w[0], Jp, Jl
+
+
+def hlm_expmap(x):
+    x = np.ascontiguousarray(x, np.float64)
+    T = np.zeros(16)
+    _hlm_lib().refhlm_expmap(_p(x), _p(T))
+    return T.reshape(4, 4)
+
+
+def hlm_logmap(T):
+    T = np.ascontiguousarray(T, np.float64).reshape(16)
+    x = np.zeros(6)
+    _hlm_lib().refhlm_logmap(_p(T), _p(x))
+    return x

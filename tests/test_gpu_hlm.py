@@ -1,0 +1,114 @@
+"""Hand-rolled LM LBA on the GPU (plba_hlm_lba) vs the CPU oracle (oracle/refhlm.cpp).
+
+MapHandler::levMarquardtOptimizationLBAForPluker (src/mapHandler.cpp:1618-2332), SURVEY.md §8f
+row 1. The oracle is a restatement (parity with the reference itself is UNPINNED, see
+oracle/refhlm.h). Bar: identical control flow (linearisations, solves, applied steps, the
+per-iteration result sequence), λ within 1e-9, and each estimate within 1e-4 of the oracle's
+total change from the initial state (the north_star 1e-4 relative bar, applied to the update so
+that windows the reference barely moves — its λ = 1e-5·max|H_ii| is ~1e19 with lines — are not
+passed trivially) plus 1e-12 of the state's magnitude.
+"""
+import numpy as np
+import pytest
+
+import oracle_api as oa
+from plba import capi, synth
+from plba.hlm import hlm_window
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def solver():
+    from plba.lib import Solver
+    s = Solver()
+    yield s
+    s.close()
+
+
+def _check_state(out, ref, init, key):
+    a, b, x0 = out[key], ref[key], init
+    if not np.size(b):
+        return
+    tol = 1e-4 * np.abs(b - x0).max() + 1e-12 * max(np.abs(b).max(), 1.0)
+    err = np.abs(a - b).max()
+    assert err <= tol, (key, err, tol)
+
+
+def _compare(out, ref, win):
+    for k in ("linearizations", "solves", "accepted"):
+        assert out[k] == ref[k], (k, out[k], ref[k])
+    tg, tr = out["trace"], ref["trace"]
+    assert len(tg) == len(tr)
+    np.testing.assert_array_equal(tg["iter"], tr["iter"])
+    np.testing.assert_array_equal(tg["result"], tr["result"])
+    np.testing.assert_allclose(tg["lambda_start"], tr["lambda_start"], rtol=1e-9)
+    np.testing.assert_allclose(tg["lambda_end"], tr["lambda_end"], rtol=1e-9)
+    if np.isfinite(ref["err"]):
+        assert out["err"] == pytest.approx(ref["err"], rel=1e-9)
+    else:
+        assert out["err"] == ref["err"] or (np.isnan(out["err"]) and np.isnan(ref["err"]))
+    assert out["dx_norm"] == pytest.approx(ref["dx_norm"], rel=1e-4, abs=1e-30)
+    g = win.graph
+    # poses compared as Tiw = inverse_se3(expmap_se3(X_i)): logmap_se3 divides by sin θ
+    # (src2/auxiliar.cpp:163), so the 6-vector of a KF whose rotation is near π carries rounding
+    # amplified by 1/sin θ on either side while the pose itself agrees
+    _check_state(out, ref, g.kf_Tcw, "kf_Tcw")
+    np.testing.assert_allclose(out["kf_x"], ref["kf_x"], rtol=0, atol=1e-6)
+    _check_state(out, ref, g.pt_xyz, "pt_xyz")
+    _check_state(out, ref, g.ln_orth, "ln_orth")
+    free = g.kf_fixed == 0
+    np.testing.assert_array_equal(out["kf_x"][~free], win.kf_x[~free])  # KFs outside kf_list untouched
+
+
+CASES = [("C1", {}), ("C1L", {}), ("C2", {}),
+         ("C1L", {"lambda0": 1e-24, "err_per_obs": 1}),
+         ("C2", {"lambda0": 1e-24, "err_per_obs": 1}),
+         ("C2", {"lambda0": 1e-24}),
+         ("C1", {"err_per_obs": 1, "max_iters": 4})]
+
+
+@pytest.mark.parametrize("cfg,params", CASES, ids=[f"{c}-{'-'.join(f'{k}={v}' for k, v in p.items()) or 'ref'}"
+                                                  for c, p in CASES])
+def test_hlm_matches_oracle(solver, cfg, params):
+    win = hlm_window(synth.generate(cfg))
+    p = capi.hlm_params(**params)
+    ref = oa.hlm_lba(win, p)
+    solver.upload(win.graph)
+    out = solver.hlm_lba(win, p)
+    _compare(out, ref, win)
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C4"])
+def test_hlm_large_windows_match_oracle(solver, cfg):
+    """C3: two-sided column-lane factorisation; C4: block cyclic reduction (pose update inside it)."""
+    win = hlm_window(synth.generate(cfg))
+    p = capi.hlm_params(lambda0=1e-24, err_per_obs=1, max_iters=6)
+    ref = oa.hlm_lba(win, p)
+    solver.upload(win.graph)
+    out = solver.hlm_lba(win, p)
+    _compare(out, ref, win)
+
+
+def test_hlm_then_g2o_on_one_context(solver):
+    """The hand-rolled loop leaves the context usable for the g2o schedule (and vice versa)."""
+    g = synth.generate("C1L")
+    win = hlm_window(g)
+    solver.upload(win.graph)
+    a = solver.hlm_lba(win)
+    b = solver.lba_plucker()
+    c = solver.hlm_lba(win)
+    ref = oa.lba_plucker(win.graph)
+    assert np.abs(b["pt_xyz"] - ref["pt_xyz"]).max() < 1e-6
+    for k in ("kf_x", "pt_xyz", "ln_orth"):
+        assert np.array_equal(a[k], c[k]), k
+
+
+def test_hlm_rerun_is_bitwise_deterministic(solver):
+    win = hlm_window(synth.generate("C2"))
+    p = capi.hlm_params(lambda0=1e-24, err_per_obs=1)
+    solver.upload(win.graph)
+    a = solver.hlm_lba(win, p)
+    b = solver.hlm_lba(win, p)
+    for k in ("kf_x", "kf_Tcw", "pt_xyz", "ln_orth"):
+        assert np.array_equal(a[k], b[k]), k
