@@ -80,6 +80,27 @@ int plslam_kf_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int3
 /* MapHandler::localBundleAdjustmentForPlukerWithG2O() */
 int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats);
 
+/* ---- MapHandler::localBundleAdjustmentForPluker() (src/mapHandler.cpp:1505-1615), the hand-rolled
+ * LM of levMarquardtOptimizationLBAForPluker (:1618-2332) on the GPU (plba_hlm_lba), and its
+ * write-back (:2160-2330: T_kf_w = expmap_se3(X_i); point3D = X with inlier = false when it moved
+ * more than 0.01; NDw = changeOrthToPluker(X − orthNDw) — the reference converts the difference).
+ * x_kf_w: KeyFrame::x_kf_w; plslam_add_keyframe initialises it to logmap_se3(T_kf_w). */
+int plslam_set_keyframe_x(plslam_map *m, int32_t kf_idx, const double x[6]);
+int plslam_get_keyframe_x(plslam_map *m, int32_t kf_idx, double x[6]);
+typedef int (*plslam_hlm_solve_fn)(void *user, const plba_graph *g, const plba_hlm_state *st,
+                                   const plba_hlm_params *p, plba_hlm_result *r);
+int plslam_set_hlm_solver(plslam_map *m, plslam_hlm_solve_fn fn, void *user);   /* NULL = plba_hlm_lba */
+/* SlamConfig / Config values (NULL = plba_hlm_default_params) and vo_status == VO_INSERTING_KF */
+int plslam_set_hlm_params(plslam_map *m, const plba_hlm_params *p, int32_t vo_inserting_kf);
+typedef struct plslam_hlm_stats {
+    int32_t ret;                            /* the reference's return value: 0 or -1                */
+    int32_t n_kf_list, n_fixed_kf, n_pt, n_ln, n_pt_obs, n_ls_obs;
+    int32_t linearizations, solves, accepted;
+    int32_t pt_outliers, ln_outliers;       /* inlier = false set by the write-back                 */
+    double  err, lambda, gather_ms, solve_ms, writeback_ms;
+} plslam_hlm_stats;
+int plslam_local_ba_plucker(plslam_map *m, plslam_hlm_stats *stats);
+
 /* ---- the rest of the Plücker local-mapping step around the LBA ---- */
 /* SlamConfig::minLMObs / minLMCovGraph / minKFLocalMap (src/slamConfig.cpp:48,61-62; defaults
  * 5 / 75 / 3) and MapHandler::max_kf_idx (include/mapHandler.h, src/mapHandler.cpp:135,173). */

@@ -56,6 +56,7 @@ int plslam_add_keyframe(plslam_map *m, int32_t kf_idx, const double T_kf_w[16], 
     auto *k = new KeyFrame();
     k->kf_idx = kf_idx;
     std::memcpy(k->T_kf_w.data(), T_kf_w, sizeof(double) * 16);
+    k->x_kf_w = logmap_se3(k->T_kf_w);  // x_kf_w = logmap_se3(T) at insertion (src/mapHandler.cpp:140,179)
     if (pt_idx) k->stereo_frame.stereo_pt_idx.assign(pt_idx, pt_idx + n_pt_feat);
     if (ls_idx) k->stereo_frame.stereo_ls_idx.assign(ls_idx, ls_idx + n_ls_feat);
     place(m->mh.map_keyframes, kf_idx, k);
@@ -185,6 +186,49 @@ int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats) {
     const int rc = m->mh.localBundleAdjustmentForPlukerWithG2O(&st);
     if (rc) return rc;
     copy_stats(st, stats);
+    return PLBA_OK;
+}
+
+int plslam_set_keyframe_x(plslam_map *m, int32_t kf_idx, const double x[6]) {
+    if (!m || !x || !slot_ok(m->mh.map_keyframes, kf_idx)) return PLBA_E_INVALID;
+    std::memcpy(m->mh.map_keyframes[kf_idx]->x_kf_w.data(), x, sizeof(double) * 6);
+    return PLBA_OK;
+}
+
+int plslam_get_keyframe_x(plslam_map *m, int32_t kf_idx, double x[6]) {
+    if (!m || !x || !slot_ok(m->mh.map_keyframes, kf_idx)) return PLBA_E_INVALID;
+    std::memcpy(x, m->mh.map_keyframes[kf_idx]->x_kf_w.data(), sizeof(double) * 6);
+    return PLBA_OK;
+}
+
+int plslam_set_hlm_solver(plslam_map *m, plslam_hlm_solve_fn fn, void *user) {
+    if (!m) return PLBA_E_INVALID;
+    m->mh.setHlmSolver(fn, user);
+    return PLBA_OK;
+}
+
+int plslam_set_hlm_params(plslam_map *m, const plba_hlm_params *p, int32_t vo_inserting_kf) {
+    if (!m) return PLBA_E_INVALID;
+    if (p) m->mh.hlm_params = *p;
+    else plba_hlm_default_params(&m->mh.hlm_params);
+    m->mh.vo_inserting_kf = vo_inserting_kf != 0;
+    return PLBA_OK;
+}
+
+int plslam_local_ba_plucker(plslam_map *m, plslam_hlm_stats *stats) {
+    if (!m) return PLBA_E_INVALID;
+    HlmStats st;
+    const int rc = m->mh.localBundleAdjustmentForPluker(&st);
+    if (rc) return rc;
+    if (stats) {
+        stats->ret = st.ret;
+        stats->n_kf_list = st.n_kf_list; stats->n_fixed_kf = st.n_fixed_kf;
+        stats->n_pt = st.n_pt; stats->n_ln = st.n_ln; stats->n_pt_obs = st.n_pt_obs; stats->n_ls_obs = st.n_ls_obs;
+        stats->linearizations = st.linearizations; stats->solves = st.solves; stats->accepted = st.accepted;
+        stats->pt_outliers = st.pt_outliers; stats->ln_outliers = st.ln_outliers;
+        stats->err = st.err; stats->lambda = st.lambda;
+        stats->gather_ms = st.gather_ms; stats->solve_ms = st.solve_ms; stats->writeback_ms = st.writeback_ms;
+    }
     return PLBA_OK;
 }
 

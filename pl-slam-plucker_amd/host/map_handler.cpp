@@ -343,6 +343,21 @@ int MapHandler::gatherWindow(Window &w) {
     return PLBA_OK;
 }
 
+int MapHandler::ensureCtx() {
+    if (!ctx_) {
+        plba_opts o;
+        if (have_opts_) o = opts_;
+        else plba_default_opts(&o);
+        const int rc = plba_create(&ctx_, &o);
+        if (rc) {
+            setError("plba_create failed (%d): no usable MI355X device", rc);
+            ctx_ = nullptr;
+            return rc;
+        }
+    }
+    return PLBA_OK;
+}
+
 int MapHandler::solve(const plba_graph &g, plba_result &r) {
     if (solve_fn_) {
         const int rc = solve_fn_(solve_user_, &g, &r);
@@ -505,6 +520,243 @@ int MapHandler::localBundleAdjustmentForPlukerWithG2O(LbaStats *stats) {
     st.gather_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     st.solve_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     st.bookkeeping_ms = std::chrono::duration<double, std::milli>(t3 - t2).count();
+    if (stats) *stats = st;
+    return PLBA_OK;
+}
+
+// ------------------------------------------------------------------ hand-rolled LM LBA (§8f row 1)
+Mat4 inverse_se3(const Mat4 &T) {  // src2/auxiliar.cpp:113-122
+    Mat4 Ti{};
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) Ti[i * 4 + j] = T[j * 4 + i];
+        Ti[i * 4 + 3] = -(T[0 * 4 + i] * T[3] + T[1 * 4 + i] * T[7] + T[2 * 4 + i] * T[11]);
+    }
+    Ti[15] = 1.0;
+    return Ti;
+}
+static void skew3(const double *v, double *M) {
+    M[0] = 0;     M[1] = -v[2]; M[2] = v[1];
+    M[3] = v[2];  M[4] = 0;     M[5] = -v[0];
+    M[6] = -v[1]; M[7] = v[0];  M[8] = 0;
+}
+static void mul3(const double *A, const double *B, double *C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) C[i * 3 + j] = A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
+}
+Mat4 expmap_se3(const Vec6 &x) {  // src2/auxiliar.cpp:124-141
+    const double w[3] = {x[3], x[4], x[5]};
+    double t[3] = {x[0], x[1], x[2]};
+    const double theta = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (!(theta < 0.000001)) {
+        double s[9], ss[9], V[9];
+        skew3(w, s);
+        for (double &v : s) v /= theta;
+        mul3(s, s, ss);
+        const double st = std::sin(theta), ct = 1.0 - std::cos(theta);
+        for (int i = 0; i < 9; ++i) {
+            const double I = (i % 4 == 0) ? 1.0 : 0.0;
+            R[i] = (I + s[i] * st) + ss[i] * ct;
+            V[i] = (I + s[i] * ct / theta) + ss[i] * (theta - st) / theta;
+        }
+        const double t0 = t[0], t1 = t[1], t2 = t[2];
+        for (int i = 0; i < 3; ++i) t[i] = V[i * 3] * t0 + V[i * 3 + 1] * t1 + V[i * 3 + 2] * t2;
+    }
+    Mat4 T{};
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) T[i * 4 + j] = R[i * 3 + j];
+        T[i * 4 + 3] = t[i];
+    }
+    T[15] = 1.0;
+    return T;
+}
+Vec6 logmap_se3(const Mat4 &T) {  // src2/auxiliar.cpp:143-173
+    const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+    double w[3] = {0, 0, 0}, V[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double cosine = (R[0] + R[4] + R[8] - 1.0) / 2.0;
+    if (cosine > 1.0) cosine = 1.0;
+    else if (cosine < -1.0) cosine = -1.0;
+    double sine = std::sqrt(1.0 - cosine * cosine);
+    if (sine > 1.0) sine = 1.0;
+    else if (sine < -1.0) sine = -1.0;
+    const double theta = std::acos(cosine);
+    if (theta > 0.000001) {
+        w[0] = theta * (R[7] - R[5]) / (2.0 * sine);
+        w[1] = theta * (R[2] - R[6]) / (2.0 * sine);
+        w[2] = theta * (R[3] - R[1]) / (2.0 * sine);
+        double s[9], ss[9];
+        skew3(w, s);
+        for (double &v : s) v /= theta;
+        mul3(s, s, ss);
+        for (int i = 0; i < 9; ++i) {
+            const double I = (i % 4 == 0) ? 1.0 : 0.0;
+            V[i] = (I + s[i] * (1.0 - cosine) / theta) + ss[i] * (theta - sine) / theta;
+        }
+    }
+    // t = V⁻¹·Vt (closed-form 3x3 inverse)
+    const double c0 = V[4] * V[8] - V[5] * V[7], c1 = V[5] * V[6] - V[3] * V[8], c2 = V[3] * V[7] - V[4] * V[6];
+    const double det = V[0] * c0 + V[1] * c1 + V[2] * c2;
+    const double Vi[9] = {c0 / det, (V[2] * V[7] - V[1] * V[8]) / det, (V[1] * V[5] - V[2] * V[4]) / det,
+                          c1 / det, (V[0] * V[8] - V[2] * V[6]) / det, (V[2] * V[3] - V[0] * V[5]) / det,
+                          c2 / det, (V[1] * V[6] - V[0] * V[7]) / det, (V[0] * V[4] - V[1] * V[3]) / det};
+    const double Vt[3] = {T[3], T[7], T[11]};
+    Vec6 x;
+    for (int i = 0; i < 3; ++i) x[i] = Vi[i * 3] * Vt[0] + Vi[i * 3 + 1] * Vt[1] + Vi[i * 3 + 2] * Vt[2];
+    x[3] = w[0]; x[4] = w[1]; x[5] = w[2];
+    return x;
+}
+
+int MapHandler::localBundleAdjustmentForPluker(HlmStats *stats) {
+    using clk = std::chrono::steady_clock;
+    HlmStats st;
+    const auto t0 = clk::now();
+    // kf_list: local KFs except KF 0, in map order (:1511-1524)
+    std::vector<KeyFrame *> kf_list;
+    for (auto *k : map_keyframes)
+        if (k && k->local && k->kf_idx != 0) kf_list.push_back(k);
+    std::vector<MapPoint *> pts;
+    std::vector<MapLine *> lns;
+    for (auto *p : map_points)
+        if (p && p->local) pts.push_back(p);  // :1527-1565
+    for (auto *l : map_lines)
+        if (l && l->local) {  // :1567-1607 (orthNDw is written here, a side effect)
+            l->orthNDw = MapLine::changePlukerToOrth(l->NDw);
+            lns.push_back(l);
+        }
+    // observations: pt_obs_list / ls_obs_list; an observation whose KF slot is NULL is skipped by
+    // the optimiser (:1652, 1741) and so never reaches the graph here
+    std::map<int, int> kf_pos;
+    std::vector<double> kf_Tcw, kf_x;
+    std::vector<uint8_t> kf_fixed;
+    std::vector<int32_t> kf_id;
+    auto add_kf = [&](KeyFrame *k, bool fixed) {
+        kf_pos[k->kf_idx] = (int)kf_id.size();
+        const Mat4 Tiw = inverse_se3(k->T_kf_w);  // Tiw = inverse_se3(T_kf_w) (:1657-1659)
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) kf_Tcw.push_back(Tiw[r * 4 + c]);
+        for (int i = 0; i < 6; ++i) kf_x.push_back(k->x_kf_w[i]);
+        kf_fixed.push_back(fixed ? 1 : 0);
+        kf_id.push_back(k->kf_idx);
+    };
+    for (auto *k : kf_list) add_kf(k, false);
+    auto observer = [&](int o) -> int {
+        if (o < 0 || o >= (int)map_keyframes.size() || !map_keyframes[o]) return -1;
+        auto it = kf_pos.find(o);
+        if (it != kf_pos.end()) return it->second;
+        add_kf(map_keyframes[o], true);
+        return (int)kf_id.size() - 1;
+    };
+    std::vector<double> pt_xyz, ept_obs, ln_orth, ln_plk, eln_obs;
+    std::vector<int32_t> pt_id, ln_id, ept_lm, ept_kf, eln_lm, eln_kf;
+    for (size_t i = 0; i < pts.size(); ++i) {
+        MapPoint *p = pts[i];
+        pt_id.push_back(p->idx);
+        for (int k = 0; k < 3; ++k) pt_xyz.push_back(p->point3D[k]);
+        for (size_t o = 0; o < p->kf_obs_list.size(); ++o) {
+            ++st.n_pt_obs;
+            const int kp = observer(p->kf_obs_list[o]);
+            if (kp < 0) continue;
+            ept_lm.push_back((int32_t)i);
+            ept_kf.push_back(kp);
+            ept_obs.push_back(p->obs_list[o][0]);
+            ept_obs.push_back(p->obs_list[o][1]);
+        }
+    }
+    for (size_t i = 0; i < lns.size(); ++i) {
+        MapLine *l = lns[i];
+        ln_id.push_back(l->idx);
+        for (int k = 0; k < 4; ++k) ln_orth.push_back(l->orthNDw[k]);
+        for (int k = 0; k < 6; ++k) ln_plk.push_back(l->NDw[k]);
+        for (size_t o = 0; o < l->kf_obs_list.size(); ++o) {
+            ++st.n_ls_obs;
+            const int kp = observer(l->kf_obs_list[o]);
+            if (kp < 0) continue;
+            eln_lm.push_back((int32_t)i);
+            eln_kf.push_back(kp);
+            for (int k = 0; k < 4; ++k) eln_obs.push_back(l->NDw_obs_list[o][k]);
+        }
+    }
+    st.n_kf_list = (int)kf_list.size();
+    st.n_fixed_kf = (int)kf_id.size() - st.n_kf_list;
+    st.n_pt = (int)pts.size();
+    st.n_ln = (int)lns.size();
+    if (st.n_pt_obs + st.n_ls_obs == 0) {  // :1610-1614
+        st.ret = -1;
+        if (stats) *stats = st;
+        return PLBA_OK;
+    }
+    std::vector<double> ept_info(ept_lm.size(), 1.0), eln_info(eln_lm.size(), 1.0);
+    plba_graph g{};
+    g.n_kf = (int32_t)kf_id.size(); g.n_pt = (int32_t)pt_id.size(); g.n_ln = (int32_t)ln_id.size();
+    g.n_ept = (int32_t)ept_lm.size(); g.n_eln = (int32_t)eln_lm.size();
+    g.fx = fx_; g.fy = fy_; g.cx = cx_; g.cy = cy_;
+    g.kf_Tcw = kf_Tcw.data(); g.kf_fixed = kf_fixed.data(); g.kf_id = kf_id.data();
+    g.pt_xyz = pt_xyz.data(); g.pt_id = pt_id.data(); g.ln_orth = ln_orth.data(); g.ln_id = ln_id.data();
+    g.ept_lm = ept_lm.data(); g.ept_kf = ept_kf.data(); g.ept_obs = ept_obs.data(); g.ept_info = ept_info.data();
+    g.eln_lm = eln_lm.data(); g.eln_kf = eln_kf.data(); g.eln_obs = eln_obs.data(); g.eln_info = eln_info.data();
+    plba_hlm_state hs{kf_x.data(), ln_plk.data()};
+    std::vector<double> x_out(kf_x.size()), T_out(kf_Tcw.size()), xyz_out(pt_xyz.size()), orth_out(ln_orth.size());
+    plba_hlm_result r{};
+    r.kf_x = x_out.data(); r.kf_Tcw = T_out.data(); r.pt_xyz = xyz_out.data(); r.ln_orth = orth_out.data();
+    const auto t1 = clk::now();
+    int rc;
+    if (hlm_fn_) {
+        rc = hlm_fn_(hlm_user_, &g, &hs, &hlm_params, &r);
+        if (rc) setError("hand-rolled LM solver hook returned %d", rc);
+    } else {
+        rc = ensureCtx();
+        if (!rc) rc = plba_upload(ctx_, &g);
+        if (!rc) rc = plba_hlm_lba(ctx_, &hs, &hlm_params, &r);
+        if (rc) setError("plba: %s", plba_last_error(ctx_));
+    }
+    if (rc) return rc;
+    const auto t2 = clk::now();
+    st.linearizations = r.linearizations; st.solves = r.solves; st.accepted = r.accepted;
+    st.err = r.err; st.lambda = r.lambda;
+    if (vo_inserting_kf) {  // :2160, 2327-2328
+        st.ret = -1;
+    } else {
+        // :2165-2198. KFs: T_kf_w = expmap_se3(X_i) (x_kf_w itself is not updated)
+        for (size_t k = 0; k < kf_list.size(); ++k) {
+            Vec6 x;
+            for (int i = 0; i < 6; ++i) x[i] = x_out[k * 6 + i];
+            kf_list[k]->T_kf_w = expmap_se3(x);
+        }
+        for (size_t i = 0; i < pts.size(); ++i) {
+            double dx[3], n2 = 0;
+            for (int k = 0; k < 3; ++k) {
+                dx[k] = xyz_out[i * 3 + k] - pts[i]->point3D[k];
+                n2 += dx[k] * dx[k];
+            }
+            if (std::sqrt(n2) > 0.01) {
+                pts[i]->inlier = false;
+                ++st.pt_outliers;
+            }
+            for (int k = 0; k < 3; ++k) pts[i]->point3D[k] = xyz_out[i * 3 + k];
+        }
+        for (size_t i = 0; i < lns.size(); ++i) {
+            // NDw = changeOrthToPluker(DX) with DX = X − orthNDw: the reference converts the
+            // difference, not the new estimate (:2190-2196) — reproduced
+            Vec4 dx;
+            double n2 = 0;
+            for (int k = 0; k < 4; ++k) {
+                dx[k] = orth_out[i * 4 + k] - lns[i]->orthNDw[k];
+                n2 += dx[k] * dx[k];
+            }
+            if (std::sqrt(n2) > 0.01) {
+                lns[i]->inlier = false;
+                ++st.ln_outliers;
+            }
+            lns[i]->NDw = MapLine::changeOrthToPluker(dx);
+        }
+        // "Remove bad observations" (:2200-2322) acts on observations flagged -1 in column 5,
+        // which nothing sets (:1549, 1591): no-op, as in the reference
+        st.ret = 0;
+    }
+    const auto t3 = clk::now();
+    st.gather_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    st.solve_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    st.writeback_ms = std::chrono::duration<double, std::milli>(t3 - t2).count();
     if (stats) *stats = st;
     return PLBA_OK;
 }

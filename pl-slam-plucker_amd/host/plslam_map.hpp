@@ -37,6 +37,8 @@ struct KeyFrame {
     bool local = false;
     int kf_idx = -1;
     Mat4 T_kf_w{};  // camera -> world
+    Vec6 x_kf_w{};  // logmap_se3 of T_kf_w at insertion (src/mapHandler.cpp:140,179); the g2o LBA
+                    // writes T_kf_w only, so this can be stale — the hand-rolled LBA reads it
     StereoFrame stereo_frame;
 };
 
@@ -66,6 +68,7 @@ struct MapLine {
     bool inlier = true;
     bool local = false;
     Vec6 NDw{};
+    Vec4 orthNDw{};  // set by localBundleAdjustmentForPluker (src/mapHandler.cpp:1577)
     Desc med_desc;
     std::vector<Desc> desc_list;
     std::vector<Vec4> NDw_obs_list;
@@ -107,6 +110,17 @@ struct LbaStats {
 };
 
 using SolveFn = int (*)(void *user, const plba_graph *g, plba_result *r);
+using HlmSolveFn = int (*)(void *user, const plba_graph *g, const plba_hlm_state *st, const plba_hlm_params *p,
+                           plba_hlm_result *r);
+
+// One localBundleAdjustmentForPluker call (hand-rolled LM).
+struct HlmStats {
+    int ret = 0;  // the reference's return value: 0, or -1 (no observations / VO inserting a KF)
+    int n_kf_list = 0, n_fixed_kf = 0, n_pt = 0, n_ln = 0, n_pt_obs = 0, n_ls_obs = 0;
+    int linearizations = 0, solves = 0, accepted = 0;
+    int pt_outliers = 0, ln_outliers = 0;  // inlier = false set by the write-back (|DX| > 0.01)
+    double err = 0, lambda = 0, gather_ms = 0, solve_ms = 0, writeback_ms = 0;
+};
 
 // The SlamConfig values the local-mapping step reads (src/slamConfig.cpp:48,61-62 defaults).
 struct SlamParams {
@@ -151,7 +165,15 @@ class MapHandler {
     // on an inconsistent map, :5894,5910,5998,6062; here the map is left untouched then).
     int localBundleAdjustmentForPlukerWithG2O(LbaStats *stats = nullptr);
 
+    // src/mapHandler.cpp:1505-1615 + levMarquardtOptimizationLBAForPluker (:1618-2332): the
+    // hand-rolled LM LBA of the Plücker map (dead code in the reference's localMappingThread,
+    // :1277, kept callable). Returns PLBA_OK (stats->ret carries the reference's 0 / -1).
+    int localBundleAdjustmentForPluker(HlmStats *stats = nullptr);
+    plba_hlm_params hlm_params{1e-5, 10.0, 1e-7, 1e-7, 1e-7, 15, 0};
+    bool vo_inserting_kf = false;  // vo_status == VO_INSERTING_KF (:2160): nothing is written back
+
     void setSolver(SolveFn fn, void *user) { solve_fn_ = fn; solve_user_ = user; }
+    void setHlmSolver(HlmSolveFn fn, void *user) { hlm_fn_ = fn; hlm_user_ = user; }
     const std::string &lastError() const { return err_; }
     void setError(const char *fmt, ...);
 
@@ -160,6 +182,7 @@ class MapHandler {
 
   private:
     int solve(const plba_graph &g, plba_result &r);
+    int ensureCtx();
     int outlierPass(Window &w, const std::vector<double> &ept_chi2, const std::vector<uint8_t> &ept_depth_ok,
                     const std::vector<uint8_t> &ept_level, const std::vector<double> &eln_chi2,
                     const std::vector<uint8_t> &eln_level, LbaStats &st);
@@ -169,11 +192,17 @@ class MapHandler {
     plba_ctx *ctx_ = nullptr;  // reused across LBA calls
     SolveFn solve_fn_ = nullptr;
     void *solve_user_ = nullptr;
+    HlmSolveFn hlm_fn_ = nullptr;
+    void *hlm_user_ = nullptr;
     std::string err_;
 };
 
 // helpers (host restatements)
 Mat4 inverse4(const Mat4 &T);  // Eigen Matrix4d::inverse (general cofactor inverse)
+// src2/auxiliar.cpp:113-173 (row-major 4x4, x = [t; ω])
+Mat4 inverse_se3(const Mat4 &T);
+Mat4 expmap_se3(const Vec6 &x);
+Vec6 logmap_se3(const Mat4 &T);
 int hamming(const Desc &a, const Desc &b);
 
 }  // namespace plslam

@@ -186,6 +186,20 @@ class PlslamLbaStats(C.Structure):
 
 
 SOLVE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(capi.PlbaGraph), C.POINTER(capi.PlbaResult))
+HLM_SOLVE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(capi.PlbaGraph), C.POINTER(capi.PlbaHlmState),
+                           C.POINTER(capi.PlbaHlmParams), C.POINTER(capi.PlbaHlmResult))
+
+
+class PlslamHlmStats(C.Structure):
+    _fields_ = [("ret", C.c_int32), ("n_kf_list", C.c_int32), ("n_fixed_kf", C.c_int32), ("n_pt", C.c_int32),
+                ("n_ln", C.c_int32), ("n_pt_obs", C.c_int32), ("n_ls_obs", C.c_int32),
+                ("linearizations", C.c_int32), ("solves", C.c_int32), ("accepted", C.c_int32),
+                ("pt_outliers", C.c_int32), ("ln_outliers", C.c_int32),
+                ("err", C.c_double), ("lambda_", C.c_double), ("gather_ms", C.c_double), ("solve_ms", C.c_double),
+                ("writeback_ms", C.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 HOST_EXPORTED = [
     "plslam_map_create", "plslam_map_destroy", "plslam_map_last_error", "plslam_set_solver", "plslam_add_keyframe",
@@ -195,6 +209,8 @@ HOST_EXPORTED = [
     "plslam_pluker_to_orth", "plslam_orth_to_pluker",
     "plslam_set_inlier", "plslam_set_params", "plslam_set_max_kf_idx", "plslam_kf_lines_idx_set", "plslam_kf_lines_idx_get",
     "plslam_form_local_map", "plslam_remove_bad_landmarks_pluker", "plslam_local_mapping_step", "plslam_exists",
+    "plslam_set_keyframe_x", "plslam_get_keyframe_x", "plslam_set_hlm_solver", "plslam_set_hlm_params",
+    "plslam_local_ba_plucker",
 ]
 
 
@@ -251,6 +267,11 @@ def load_host(path: Optional[str] = None):
     L.plslam_remove_bad_landmarks_pluker.argtypes = [vp, ip, ip]
     L.plslam_local_mapping_step.argtypes = [vp, C.c_int32, C.POINTER(PlslamLbaStats), ip, ip]
     L.plslam_exists.argtypes = [vp, C.c_int32, C.c_int32, ip]
+    L.plslam_set_keyframe_x.argtypes = [vp, C.c_int32, dp]
+    L.plslam_get_keyframe_x.argtypes = [vp, C.c_int32, dp]
+    L.plslam_set_hlm_solver.argtypes = [vp, HLM_SOLVE_FN, vp]
+    L.plslam_set_hlm_params.argtypes = [vp, C.POINTER(capi.PlbaHlmParams), C.c_int32]
+    L.plslam_local_ba_plucker.argtypes = [vp, C.POINTER(PlslamHlmStats)]
     for n in HOST_EXPORTED:
         if n not in ("plslam_map_last_error", "plslam_pluker_to_orth", "plslam_orth_to_pluker"):
             getattr(L, n).restype = C.c_int
@@ -373,6 +394,42 @@ class HostMap:
         st = PlslamLbaStats()
         self._check(self.L.plslam_local_ba_plucker_g2o(self.h, C.byref(st)), "local_ba_plucker_g2o")
         return st.as_dict()
+
+    # -- hand-rolled LM LBA (MapHandler::localBundleAdjustmentForPluker)
+    def set_hlm_solver(self, fn: Optional[Callable]):
+        """fn(graph, state, params, result) -> int, or None for the MI355X backend (plba_hlm_lba)."""
+        if fn is None:
+            self._hcb = None
+            self._check(self.L.plslam_set_hlm_solver(self.h, C.cast(None, HLM_SOLVE_FN), None), "set_hlm_solver")
+            return
+
+        def tramp(user, gp, sp, pp, rp):
+            try:
+                return int(fn(gp.contents, sp.contents, pp.contents, rp.contents))
+            except Exception:  # never unwind through C
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._hcb = HLM_SOLVE_FN(tramp)
+        self._check(self.L.plslam_set_hlm_solver(self.h, self._hcb, None), "set_hlm_solver")
+
+    def set_hlm_params(self, params=None, vo_inserting_kf: bool = False):
+        self._check(self.L.plslam_set_hlm_params(self.h, C.byref(params) if params is not None else None,
+                                                 int(vo_inserting_kf)), "set_hlm_params")
+
+    def local_ba_hlm(self) -> dict:
+        st = PlslamHlmStats()
+        self._check(self.L.plslam_local_ba_plucker(self.h, C.byref(st)), "local_ba_plucker")
+        return st.as_dict()
+
+    def keyframe_x(self, kf_idx: int) -> np.ndarray:
+        x = np.zeros(6)
+        self._check(self.L.plslam_get_keyframe_x(self.h, kf_idx, x.ctypes.data_as(C.POINTER(C.c_double))), "get_x")
+        return x
+
+    def set_keyframe_x(self, kf_idx: int, x):
+        a, ap = _d(x)
+        self._check(self.L.plslam_set_keyframe_x(self.h, kf_idx, ap), "set_x")
 
     def form_local_map(self, kf_idx: int):
         self._check(self.L.plslam_form_local_map(self.h, kf_idx), "form_local_map")
