@@ -388,6 +388,109 @@ int collect_timing(plba_ctx *ctx) {
 
 
 // ------------------------------------------------------------------ upload / structure prep
+// Reverse Cuthill–McKee order of the free poses (hidx 0..nf-1) on the graph "two free poses
+// observe a common landmark": BFS from a pseudo-peripheral vertex of each component, neighbours
+// by increasing degree, then reversed. Returns rcm[i] = the hidx placed at position i.
+std::vector<int32_t> rcm_order(const plba_graph *g, const std::vector<int32_t> &kf_hidx, int nf) {
+    const int nl = g->n_pt + g->n_ln;
+    std::vector<std::vector<int32_t>> lm_poses(nl);
+    for (int e = 0; e < g->n_ept; ++e) {
+        const int h = kf_hidx[g->ept_kf[e]];
+        if (h >= 0) lm_poses[g->ept_lm[e]].push_back(h);
+    }
+    for (int e = 0; e < g->n_eln; ++e) {
+        const int h = kf_hidx[g->eln_kf[e]];
+        if (h >= 0) lm_poses[g->n_pt + g->eln_lm[e]].push_back(h);
+    }
+    std::vector<std::vector<int32_t>> adj(nf);
+    for (auto &v : lm_poses) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (size_t i = 0; i < v.size(); ++i)
+            for (size_t j = i + 1; j < v.size(); ++j) {
+                adj[v[i]].push_back(v[j]);
+                adj[v[j]].push_back(v[i]);
+            }
+    }
+    std::vector<int32_t> deg(nf);
+    for (int h = 0; h < nf; ++h) {
+        auto &a = adj[h];
+        std::sort(a.begin(), a.end());
+        a.erase(std::unique(a.begin(), a.end()), a.end());
+        deg[h] = (int32_t)a.size();
+    }
+    for (int h = 0; h < nf; ++h)
+        std::stable_sort(adj[h].begin(), adj[h].end(), [&](int x, int y) { return deg[x] < deg[y]; });
+    std::vector<int32_t> order;
+    order.reserve(nf);
+    std::vector<char> seen(nf, 0);
+    auto bfs = [&](int root, std::vector<int32_t> &out) {  // returns the last level's min-degree vertex
+        std::vector<int32_t> lev(nf, -1);
+        out.clear();
+        out.push_back(root);
+        lev[root] = 0;
+        for (size_t q = 0; q < out.size(); ++q)
+            for (int v : adj[out[q]])
+                if (lev[v] < 0) {
+                    lev[v] = lev[out[q]] + 1;
+                    out.push_back(v);
+                }
+        const int last = lev[out.back()];
+        int best = out.back();
+        for (int v : out)
+            if (lev[v] == last && deg[v] < deg[best]) best = v;
+        return std::make_pair(best, last);
+    };
+    std::vector<int32_t> comp;
+    for (int s0 = 0; s0 < nf; ++s0) {
+        if (seen[s0]) continue;
+        // pseudo-peripheral start: repeat BFS from the far end while the depth grows
+        int root = s0;
+        auto r = bfs(root, comp);
+        for (int it = 0; it < 8; ++it) {
+            auto r2 = bfs(r.first, comp);
+            if (r2.second <= r.second) break;
+            root = r.first;
+            r = r2;
+        }
+        bfs(root, comp);  // Cuthill–McKee order of this component (neighbours by degree)
+        for (int v : comp) {
+            seen[v] = 1;
+            order.push_back(v);
+        }
+    }
+    std::reverse(order.begin(), order.end());
+    // refinement: a few passes of "sort by the mean position of self and neighbours" (a discrete
+    // smoothing that straightens thick paths, where level-by-level orders give ~2x the band);
+    // the narrowest order seen wins
+    auto bandwidth = [&](const std::vector<int32_t> &ord) {
+        std::vector<int32_t> p(nf);
+        for (int i = 0; i < nf; ++i) p[ord[i]] = i;
+        int w = 0;
+        for (int h = 0; h < nf; ++h)
+            for (int v : adj[h]) w = std::max(w, std::abs(p[h] - p[v]));
+        return w;
+    };
+    std::vector<int32_t> best = order, cur = order, p(nf);
+    int bw_best = bandwidth(best);
+    for (int it = 0; it < 24 && bw_best > 0; ++it) {
+        for (int i = 0; i < nf; ++i) p[cur[i]] = i;
+        std::vector<double> key(nf);
+        for (int h = 0; h < nf; ++h) {
+            double s = p[h];
+            for (int v : adj[h]) s += p[v];
+            key[h] = s / (double)(adj[h].size() + 1);
+        }
+        std::stable_sort(cur.begin(), cur.end(), [&](int a, int b) { return key[a] < key[b]; });
+        const int w = bandwidth(cur);
+        if (w < bw_best) {
+            bw_best = w;
+            best = cur;
+        }
+    }
+    return best;
+}
+
 int do_upload(plba_ctx *ctx, const plba_graph *g) {
     if (!g || g->n_kf < 0 || g->n_pt < 0 || g->n_ln < 0 || g->n_ept < 0 || g->n_eln < 0) {
         ctx->set_error("invalid graph sizes");
@@ -474,6 +577,48 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     int nf = 0;
     for (int k : korder)
         if (!g->kf_fixed[k]) kf_hidx[k] = nf++;
+    std::vector<int32_t> first_blk(nf);
+    auto envelope = [&](const std::vector<int32_t> &hidx, std::vector<int32_t> &fb) {
+        for (int h = 0; h < nf; ++h) fb[h] = h;
+        std::vector<int32_t> lmin(n_pt_g + n_ln_g, INT32_MAX);
+        for (int e = 0; e < Ep_g; ++e) {
+            const int h = hidx[g->ept_kf[e]];
+            if (h >= 0) lmin[g->ept_lm[e]] = std::min(lmin[g->ept_lm[e]], h);
+        }
+        for (int e = 0; e < El_g; ++e) {
+            const int h = hidx[g->eln_kf[e]];
+            if (h >= 0) lmin[n_pt_g + g->eln_lm[e]] = std::min(lmin[n_pt_g + g->eln_lm[e]], h);
+        }
+        for (int e = 0; e < Ep_g; ++e) {
+            const int h = hidx[g->ept_kf[e]];
+            if (h >= 0) fb[h] = std::min(fb[h], lmin[g->ept_lm[e]]);
+        }
+        for (int e = 0; e < El_g; ++e) {
+            const int h = hidx[g->eln_kf[e]];
+            if (h >= 0) fb[h] = std::min(fb[h], lmin[n_pt_g + g->eln_lm[e]]);
+        }
+        int w = 0;
+        for (int h = 0; h < nf; ++h) w = std::max(w, h - fb[h]);
+        return w;
+    };
+    int bw = envelope(kf_hidx, first_blk);
+    // Reverse Cuthill–McKee on the free-pose coupling graph when the natural (id) order leaves an
+    // envelope wider than the column-lane / BCR kernels take: windows that revisit old keyframes
+    // couple poses a loop apart. LinearSolverEigen orders the same matrix by AMD; any symmetric
+    // permutation gives the same exact LDLᵀ solution (rounding aside). PLBA_NO_RCM=1 disables.
+    if (bw > kClMaxBW && nf > 2 && !env_flag("PLBA_NO_RCM")) {
+        std::vector<int32_t> rcm = rcm_order(g, kf_hidx, nf);
+        std::vector<int32_t> pos(nf), h2(n_kf, -1), fb2(nf);
+        for (int i = 0; i < nf; ++i) pos[rcm[i]] = i;
+        for (int k = 0; k < n_kf; ++k) h2[k] = kf_hidx[k] >= 0 ? pos[kf_hidx[k]] : -1;
+        const int bw2 = envelope(h2, fb2);
+        if (bw2 < bw) {
+            kf_hidx = h2;
+            first_blk = fb2;
+            bw = bw2;
+        }
+    }
+    mark("envelope (+ RCM)");
 
     // landmark-major CSR of the local landmarks (stable within a landmark = g2o insertion order)
     std::vector<int32_t> lm_cnt(n_lm + 1, 0);
@@ -531,29 +676,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // all-reduced value array must have one layout). Blocks are indexed densely within the
     // envelope in (i2, i1) order; Schur triples (e1 at pose i1 <= e2 at pose i2, same landmark,
     // local landmarks only) are counting-sorted by block, landmark order inside a block.
-    std::vector<int32_t> first_blk(nf);
-    for (int h = 0; h < nf; ++h) first_blk[h] = h;
-    {
-        std::vector<int32_t> lmin(n_pt_g + n_ln_g, INT32_MAX);
-        for (int e = 0; e < Ep_g; ++e) {
-            const int h = kf_hidx[g->ept_kf[e]];
-            if (h >= 0) lmin[g->ept_lm[e]] = std::min(lmin[g->ept_lm[e]], h);
-        }
-        for (int e = 0; e < El_g; ++e) {
-            const int h = kf_hidx[g->eln_kf[e]];
-            if (h >= 0) lmin[n_pt_g + g->eln_lm[e]] = std::min(lmin[n_pt_g + g->eln_lm[e]], h);
-        }
-        for (int e = 0; e < Ep_g; ++e) {
-            const int h = kf_hidx[g->ept_kf[e]];
-            if (h >= 0) first_blk[h] = std::min(first_blk[h], lmin[g->ept_lm[e]]);
-        }
-        for (int e = 0; e < El_g; ++e) {
-            const int h = kf_hidx[g->eln_kf[e]];
-            if (h >= 0) first_blk[h] = std::min(first_blk[h], lmin[n_pt_g + g->eln_lm[e]]);
-        }
-    }
-    int bw = 0;
-    for (int h = 0; h < nf; ++h) bw = std::max(bw, h - first_blk[h]);
     // PLBA_FORCE_DENSE=1 (diagnostics only) routes a narrow envelope through the dense path.
     const char *force_dense = getenv("PLBA_FORCE_DENSE");
     const bool band_mode = bw <= kBandMax && !(force_dense && force_dense[0] == '1');
@@ -642,6 +764,9 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.E_g = Ep_g + El_g;
     d.bw = bw;
     d.band_mode = band_mode ? 1 : 0;
+    // dense RCS: multi-workgroup blocked LDLᵀ with MFMA trailing updates; PLBA_DENSE_SCALAR=1
+    // selects the single-workgroup scalar k_rcs_factor (A/B runs)
+    d.dense_mfma = !band_mode && !env_flag("PLBA_DENSE_SCALAR") ? 1 : 0;
     d.ring = band_ring(bw, nf);
     // two-sided factorisation when the chain is long enough to halve and the separator's dense
     // system fits next to the band window in LDS (PLBA_NO_TWIST=1 disables, diagnostics only)
@@ -882,8 +1007,19 @@ int launch_step(plba_ctx *ctx) {
         }
         if (!(d.fold && d.nch > 0))  // (folded into the last chunk of each block otherwise)
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
-        if (d.band_mode) LAUNCH(K_FACTOR, launch_band(d, s));
-        else LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
+        if (d.band_mode) {
+            LAUNCH(K_FACTOR, launch_band(d, s));
+        } else if (d.dense_mfma) {  // blocked LDLᵀ, MFMA trailing updates (plba_dense.hpp)
+            for (int K = 0; K < d.ntiles; ++K) {
+                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_dense_panel, dim3(d.ntiles - K), dim3(kDensePanelNT), 0, s, d, K));
+                const int m = d.ntiles - K - 1;
+                if (m > 0)
+                    LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, d, K));
+            }
+            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_dense_solve, dim3(1), dim3(kFacThreads), 0, s, d));
+        } else {
+            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
+        }
     }
     // the factorisation kernels end with the pose update; without free poses it runs alone
     if (d.n == 0 && d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(1), dim3(kBlock), 0, s, d));
@@ -1468,10 +1604,11 @@ int plba_debug_bcr_stamps(plba_ctx *ctx, unsigned long long *out, int32_t cap, i
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[15] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+    const int64_t v[16] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
-                           ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N};
-    for (int i = 0; i < cap && i < 15; ++i) out[i] = v[i];
+                           ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N,
+                           ctx->d.dense_mfma};
+    for (int i = 0; i < cap && i < 16; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

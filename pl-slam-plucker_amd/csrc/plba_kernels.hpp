@@ -116,6 +116,7 @@ struct Dev {
     int32_t *tile_last;                 // [ntiles] last row tile whose envelope reaches column tile K
     // block-band storage (used when the envelope bandwidth bw <= kBandMax)
     int32_t bw, band_mode;              // bandwidth in pose blocks; 1 = banded factorisation
+    int32_t dense_mfma;                 // dense RCS on many workgroups + MFMA (plba_dense.hpp)
     int32_t ring;                       // steps of L / S^-1 / z staged in LDS between global flushes
     unsigned long long *stamps;         // diagnostic build only (PLBA_STAMPS): per-phase cycle sums
     int32_t *first_blk;                 // [nf] first block column of each block row (lower)
@@ -829,9 +830,79 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
     for (int i = threadIdx.x; i < d.n_ps; i += NT) d.part_ps[i] = i == 0 ? s : 0.0;
 }
 
+constexpr int kFacThreads = 1024;
+// ---- solve L D Lᵀ x = b_s through the envelope-aware dense factor in Ad (unit L below the
+// diagonal, D on it), tile by tile; one workgroup of kFacThreads. x -> xp.
+__device__ __noinline__ void dense_solve_wg(const Dev &d) {
+    __shared__ double red[kFacThreads / kTile][kTile + 1];
+    const int tid = threadIdx.x;
+    const int n = d.n;
+    const int nt = d.ntiles;
+    const double *Ad = d.Ad;
+    double *y = d.Wbuf;  // reuse: y[0..n)
+    for (int i = tid; i < n; i += kFacThreads) y[i] = d.bs[i];
+    __syncthreads();
+    // forward: tile by tile
+    for (int K = 0; K < nt; ++K) {
+        const int k0 = K * kTile, kb = min(kTile, n - k0);
+        if (tid < 64) {  // one wave solves the diagonal tile
+            double yi = (tid < kb) ? y[k0 + tid] : 0.0;
+            for (int j = 0; j < kb; ++j) {
+                const double yj = __shfl(yi, j, 64);
+                if (tid > j && tid < kb) yi -= Ad[(size_t)(k0 + tid) + (size_t)(k0 + j) * n] * yj;
+            }
+            if (tid < kb) y[k0 + tid] = yi;
+        }
+        __syncthreads();
+        const int fend = min(n, (d.tile_last[K] + 1) * kTile);
+        for (int i = k0 + kb + tid; i < fend; i += kFacThreads) {
+            if (d.tile_first[i / kTile] > K) continue;
+            double s = 0.0;
+            for (int p = 0; p < kb; ++p) s += Ad[(size_t)i + (size_t)(k0 + p) * n] * y[k0 + p];
+            y[i] -= s;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += kFacThreads) y[i] = y[i] / Ad[(size_t)i + (size_t)i * n];
+    __syncthreads();
+    // backward: Lᵀ x = y, tile by tile from the bottom
+    for (int K = nt - 1; K >= 0; --K) {
+        const int k0 = K * kTile, kb = min(kTile, n - k0);
+        // y_K -= Σ_{i > tile} L[i][k] y[i]   (column k of L below the tile): 32 partial sums per
+        // column (rows i ≡ part mod 32), added in part order
+        const int bend = min(n, (d.tile_last[K] + 1) * kTile);
+        {
+            const int c = tid % kTile, part = tid / kTile;
+            double s = 0.0;
+            if (c < kb)
+                for (int i = k0 + kb + part; i < bend; i += kFacThreads / kTile) {
+                    if (d.tile_first[i / kTile] > K) continue;
+                    s += Ad[(size_t)i + (size_t)(k0 + c) * n] * y[i];
+                }
+            red[part][c] = s;
+        }
+        __syncthreads();
+        if (tid < kb) {
+            double s = 0.0;
+            for (int p = 0; p < kFacThreads / kTile; ++p) s += red[p][tid];
+            y[k0 + tid] -= s;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            double yi = (tid < kb) ? y[k0 + tid] : 0.0;
+            for (int j = kb - 1; j >= 0; --j) {
+                const double yj = __shfl(yi, j, 64);
+                if (tid < j) yi -= Ad[(size_t)(k0 + j) + (size_t)(k0 + tid) * n] * yj;
+            }
+            if (tid < kb) y[k0 + tid] = yi;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += kFacThreads) d.xp[i] = y[i];
+}
+
 // Envelope-aware tiled LDLᵀ of the lower triangle + solve, one workgroup of 1024 threads.
 // Semantics of Eigen::SimplicialLDLT as used by LinearSolverEigen: fails iff a pivot is 0.
-constexpr int kFacThreads = 1024;
 __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
     TRIAL_GUARD
     __shared__ double T[kTile][kTile + 1];
@@ -918,60 +989,7 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
     }
     __syncthreads();
     if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
-    if (!s_fail) {  // on failure x_p keeps its previous value (g2o leaves _x untouched)
-    // ---- solve L D Lᵀ x = b_s
-    double *y = d.Wbuf;  // reuse: y[0..n)
-    for (int i = tid; i < n; i += kFacThreads) y[i] = d.bs[i];
-    __syncthreads();
-    // forward: tile by tile
-    for (int K = 0; K < nt; ++K) {
-        const int k0 = K * kTile, kb = min(kTile, n - k0);
-        if (tid < 64) {  // one wave solves the diagonal tile
-            double yi = (tid < kb) ? y[k0 + tid] : 0.0;
-            for (int j = 0; j < kb; ++j) {
-                const double yj = __shfl(yi, j, 64);
-                if (tid > j && tid < kb) yi -= Ad[(size_t)(k0 + tid) + (size_t)(k0 + j) * n] * yj;
-            }
-            if (tid < kb) y[k0 + tid] = yi;
-        }
-        __syncthreads();
-        const int fend = min(n, (d.tile_last[K] + 1) * kTile);
-        for (int i = k0 + kb + tid; i < fend; i += kFacThreads) {
-            if (d.tile_first[i / kTile] > K) continue;
-            double s = 0.0;
-            for (int p = 0; p < kb; ++p) s += Ad[(size_t)i + (size_t)(k0 + p) * n] * y[k0 + p];
-            y[i] -= s;
-        }
-        __syncthreads();
-    }
-    for (int i = tid; i < n; i += kFacThreads) y[i] = y[i] / Ad[(size_t)i + (size_t)i * n];
-    __syncthreads();
-    // backward: Lᵀ x = y, tile by tile from the bottom
-    for (int K = nt - 1; K >= 0; --K) {
-        const int k0 = K * kTile, kb = min(kTile, n - k0);
-        // y_K -= Σ_{i > tile} L[i][k] y[i]   (column k of L below the tile)
-        const int bend = min(n, (d.tile_last[K] + 1) * kTile);
-        for (int c = tid; c < kb; c += kFacThreads) {
-            double s = 0.0;
-            for (int i = k0 + kb; i < bend; ++i) {
-                if (d.tile_first[i / kTile] > K) continue;
-                s += Ad[(size_t)i + (size_t)(k0 + c) * n] * y[i];
-            }
-            y[k0 + c] -= s;
-        }
-        __syncthreads();
-        if (tid < 64) {
-            double yi = (tid < kb) ? y[k0 + tid] : 0.0;
-            for (int j = kb - 1; j >= 0; --j) {
-                const double yj = __shfl(yi, j, 64);
-                if (tid < j) yi -= Ad[(size_t)(k0 + j) + (size_t)(k0 + tid) * n] * yj;
-            }
-            if (tid < kb) y[k0 + tid] = yi;
-        }
-        __syncthreads();
-    }
-    for (int i = tid; i < n; i += kFacThreads) d.xp[i] = y[i];
-    }
+    if (!s_fail) dense_solve_wg(d);  // on failure x_p keeps its previous value (g2o leaves _x untouched)
     __syncthreads();
     pose_update_wg<kFacThreads>(d);  // the update is applied even after a failed solve (A13)
 }
@@ -1601,6 +1619,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d) {
 
 #include "plba_band_cl.hpp"
 #include "plba_bcr.hpp"
+#include "plba_dense.hpp"
 
 // ---------------------------------------------------------------- update + trial evaluation
 // stand-alone pose update (windows without free poses: no factorisation kernel to fuse into)

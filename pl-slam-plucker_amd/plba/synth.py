@@ -45,7 +45,14 @@ CONFIGS: Dict[str, tuple] = {
     "C3": (100, 20000, 4000, 1003),
     "C4": (400, 80000, 16000, 1004),
     "C5": (1000, 200000, 40000, 1005),
+    # "revisit" windows: the trajectory closes its loop (period ≈126 KFs) and a share of the
+    # landmarks is re-observed one loop later, so poses ~126 apart share landmarks and the
+    # reduced camera system loses its narrow band (the dense / reordered factorisation paths)
+    "C2R": (150, 3000, 600, 1012),
+    "C3R": (160, 20000, 4000, 1013),
 }
+REVISIT_PERIOD = 126          # 2π / 0.05 rad per KF (_trajectory)
+REVISIT_FRAC = 0.15
 
 HUBER_DELTA = float(np.float32(math.sqrt(5.991)))  # const float thHuberMono (src/mapHandler.cpp:5978)
 CHI2_THRESHOLD = 5.991                              # src/mapHandler.cpp:6129,6142
@@ -188,8 +195,13 @@ def _sample_anchor(rng, Rwc, pwc, s, L, cam, depth_lo=2.0, depth_hi=8.0, margin=
 def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int] = None,
              n_ln: Optional[int] = None, seed: Optional[int] = None, fixed_frac: float = 0.1,
              noise_px: float = 1.0, outlier_frac: float = 0.02, perturb: bool = True,
-             track_min: int = 2, track_max: int = 8) -> Graph:
-    """Generate one window. ``name`` picks a config; keyword args override it."""
+             track_min: int = 2, track_max: int = 8, revisit_frac: Optional[float] = None,
+             revisit_period: int = REVISIT_PERIOD) -> Graph:
+    """Generate one window. ``name`` picks a config; keyword args override it.
+
+    ``revisit_frac`` (default REVISIT_FRAC for the ``*R`` configs, else 0): that share of the
+    point landmarks gets one more observation from the KF one loop (``revisit_period`` KFs) after
+    the middle of its track, when that KF sees the point."""
     base = CONFIGS.get(name, (10, 500, 0, 1000))
     n_kf = base[0] if n_kf is None else n_kf
     n_pt = base[1] if n_pt is None else n_pt
@@ -247,11 +259,25 @@ def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int
     gt_plk = geo.pluker_from_endpoints(seg[:, 0], seg[:, 1]) if n_ln else np.zeros((0, 6))
     gt_orth = geo.pluker_to_orth(gt_plk) if n_ln else np.zeros((0, 4))
 
-    # ---------------- point edges (landmark-major, track order)
+    # ---------------- point edges (landmark-major, track order; a revisit observation last)
+    if revisit_frac is None:
+        revisit_frac = REVISIT_FRAC if name.endswith("R") else 0.0
     E_p = int(pt_L.sum())
     ept_lm = np.repeat(np.arange(n_pt, dtype=np.int32), pt_L)
     offs = np.arange(E_p) - np.repeat(np.cumsum(pt_L) - pt_L, pt_L)
     ept_kf = (np.repeat(pt_s, pt_L) + offs).astype(np.int32)
+    if revisit_frac > 0 and n_pt:
+        kr = pt_s + pt_L // 2 + revisit_period
+        cand = (rng.random(n_pt) < revisit_frac) & (kr < n_kf)
+        krc = np.where(cand, kr, 0)
+        u, v, z = _project(Rcw[krc], tcw[krc], gt_xyz, cam)
+        cand &= (z > 0.5) & (u >= 5) & (u < cam["width"] - 5) & (v >= 5) & (v < cam["height"] - 5)
+        extra = np.nonzero(cand)[0]
+        if extra.size:
+            ends = np.cumsum(pt_L)
+            ept_lm = np.insert(ept_lm, ends[extra], extra.astype(np.int32))
+            ept_kf = np.insert(ept_kf, ends[extra], krc[extra].astype(np.int32))
+            E_p = int(ept_lm.size)
     u, v, _ = _project(Rcw[ept_kf], tcw[ept_kf], gt_xyz[ept_lm], cam)
     ept_obs = np.stack([u, v], -1) + rng.normal(0.0, noise_px, (E_p, 2))
     ept_outlier = rng.random(E_p) < outlier_frac
