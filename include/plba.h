@@ -161,6 +161,7 @@ int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *la
 typedef struct plba_hlm_state {
     const double *kf_x;        /* [n_kf][6] KeyFrame::x_kf_w = X_aux pose blocks [t; ω] (:1518)   */
     const double *ln_pluker;   /* [n_ln][6] MapLine::NDw of the map (first linearisation, :1744)  */
+    const double *ln_line3d;   /* GBA only: [n_ln][6] MapLine::line3D endpoints [P; Q] (:3089)    */
 } plba_hlm_state;
 
 typedef struct plba_hlm_params {
@@ -173,7 +174,20 @@ typedef struct plba_hlm_params {
     int32_t err_per_obs;       /* 0 = the reference: err /= (Npt_obs + Nls_obs), both counters stay
                                   0 (:1642,1731,1849) so err becomes +inf and every step after the
                                   first is accepted; 1 = divide by the observation count instead */
+    int32_t variant;           /* PLBA_HLM_LBA_PLUCKER or PLBA_HLM_GBA                            */
+    int32_t pad;
 } plba_hlm_params;
+
+/* plba_hlm_params.variant
+ * PLBA_HLM_GBA = MapHandler::levMarquardtOptimizationGBA (src/mapHandler.cpp:3128-3726, window of
+ * globalBundleAdjustment :3022-3126): every KF but kf_idx 0 free; lines are 6-dim landmarks, the
+ * endpoints line3D = [P; Q] (state_ln_line3d), observed as image line equations (a, b, c) in
+ * eln_obs[.][0..2]; residual e = (l·π(P), l·π(Q)); from the second linearisation on both
+ * endpoints are read from X at the aliased offset 6Nkf+3Npt+3·j (:3547-3548); Hmax is an int
+ * (:3386, truncation); the stop tests use numeric_limits<double>::epsilon() (pass it as
+ * min_error / min_error_change). */
+#define PLBA_HLM_LBA_PLUCKER 0
+#define PLBA_HLM_GBA         1
 
 typedef struct plba_hlm_result {
     double  *kf_x;             /* [n_kf][6] X pose blocks at exit (KFs not in kf_list: input x)   */
@@ -189,6 +203,7 @@ typedef struct plba_hlm_result {
     double   lambda;           /* λ at exit                                                       */
     double   dx_norm;          /* ‖DX‖ of the last solve                                          */
     double   solve_ms;         /* wall time of the loop                                           */
+    double  *ln_line3d;        /* GBA: [n_ln][6] line3D at exit                                   */
 } plba_hlm_result;
 
 void plba_hlm_default_params(plba_hlm_params *p);

@@ -24,6 +24,10 @@
 //   * pose update X_i ← logmap_se3(expmap_se3(X_i)·inverse_se3(expmap_se3(DX_i))) (:1868-1873);
 //     lines updateOrthCoord (include/mapHandler.h:252-309), points X += DX.
 // The write-back and outlier bookkeeping of :2160-2330 are host-side (host/map_handler.cpp).
+// params.variant = PLBA_HLM_GBA restates MapHandler::levMarquardtOptimizationGBA (:3128-3726) the
+// same way: 6-dim endpoint lines observed as image line equations (gba_line_obs), the aliased
+// Pwj = Qwj = X.block(6Nkf+3Npt+3·j) reads after the first linearisation (:3547-3548), an int
+// Hmax (:3386), X += DX for every landmark and the ε stop tests passed in as min_error(_change).
 
 #include "refhlm.h"
 
@@ -310,6 +314,45 @@ void line_obs(const double Tcw[12], const double L[6], const double obs[4], cons
     w = 1.0 / (1.0 + r * r);
 }
 
+// ---- one GBA line observation (src/mapHandler.cpp:3270-3340 / :3545-3619): endpoints P, Q,
+// image line l = (a, b, c), e = (l·π(P), l·π(Q)); the Jacobians use fx·e0 and fy·e1 where the
+// point rows use fx·dx and fy·dy (lx = l_err(0), ly = l_err(1), :3293-3296)
+void gba_line_obs(const double Tcw[12], const double P[3], const double Q[3], const double lo[3], const Cam &c,
+                  double hth, double &r, double &w, double Jp[6], double Jl[6]) {
+    const double R[9] = {Tcw[0], Tcw[1], Tcw[2], Tcw[4], Tcw[5], Tcw[6], Tcw[8], Tcw[9], Tcw[10]};
+    double Pi[3], Qi[3];
+    mat3vec(R, P, Pi);
+    mat3vec(R, Q, Qi);
+    for (int k = 0; k < 3; ++k) {
+        Pi[k] += Tcw[4 * k + 3];
+        Qi[k] += Tcw[4 * k + 3];
+    }
+    const double pu = c.cx + c.fx * Pi[0] / Pi[2], pv = c.cy + c.fy * Pi[1] / Pi[2];
+    const double qu = c.cx + c.fx * Qi[0] / Qi[2], qv = c.cy + c.fy * Qi[1] / Qi[2];
+    const double e0 = lo[0] * pu + lo[1] * pv + lo[2];
+    const double e1 = lo[0] * qu + lo[1] * qv + lo[2];
+    r = std::sqrt(e0 * e0 + e1 * e1);
+    const double fxlx = c.fx * e0, fyly = c.fy * e1;
+    const double m = std::max(hth, r);
+    double JPi[6], JQi[6];
+    auto rows = [&](const double *G, double *Jpose, double *Jlm, double ek) {
+        const double gx = G[0], gy = G[1], gz = G[2];
+        const double gz2 = 1.0 / std::max(hth, gz * gz);
+        Jpose[0] = gz2 * fxlx * gz;
+        Jpose[1] = gz2 * fyly * gz;
+        Jpose[2] = -gz2 * (fxlx * gx + fyly * gy);
+        Jpose[3] = -gz2 * (fxlx * gx * gy + fyly * gy * gy + fyly * gz * gz);
+        Jpose[4] = gz2 * (fxlx * gx * gx + fxlx * gz * gz + fyly * gx * gy);
+        Jpose[5] = gz2 * (fyly * gx * gz - fxlx * gy * gz);
+        const double j0 = gz2 * fxlx * gz, j1 = gz2 * fyly * gz, j2 = -gz2 * (fxlx * gx + fyly * gy);
+        for (int k = 0; k < 3; ++k) Jlm[k] = ((j0 * R[k] + j1 * R[3 + k] + j2 * R[6 + k]) * ek) / m;
+    };
+    rows(Pi, JPi, Jl, e0);
+    rows(Qi, JQi, Jl + 3, e1);
+    for (int k = 0; k < 6; ++k) Jp[k] = (JPi[k] * e0 + JQi[k] * e1) / m;
+    w = 1.0 / (1.0 + r * r);
+}
+
 // ---- unpivoted LDLᵀ solve of a dense symmetric system (lower triangle read), in place
 bool ldlt_solve(std::vector<double> &A, int n, std::vector<double> &b) {
     std::vector<double> Dv(n);
@@ -334,7 +377,7 @@ bool ldlt_solve(std::vector<double> &A, int n, std::vector<double> &b) {
 
 struct Obs {
     int lm, kf, h;  // landmark (local), keyframe, free-pose index or -1
-    double r, w, Jp[6], Jl[4];
+    double r, w, Jp[6], Jl[6];
 };
 
 }  // namespace
@@ -354,15 +397,19 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
     int nf = 0;
     for (int k : korder)
         if (!g->kf_fixed[k]) hidx[k] = nf++;
-    const int N = 6 * nf + 3 * n_pt + 4 * n_ln;
-    // state X: pose blocks, points, lines (orth)
-    std::vector<double> xk((size_t)n_kf * 6), Tcw((size_t)n_kf * 12), Xp((size_t)n_pt * 3), Xl((size_t)n_ln * 4);
+    // GBA (src/mapHandler.cpp:3128-3726): lines are 6-dim endpoint landmarks line3D = [P; Q]
+    const bool gba = p->variant == PLBA_HLM_GBA;
+    if (gba && n_ln && !st->ln_line3d) return -1;
+    const int LD = gba ? 6 : 4;  // line landmark dimension
+    const int N = 6 * nf + 3 * n_pt + LD * n_ln;
+    // state X: pose blocks, points, lines (orth, or GBA endpoints)
+    std::vector<double> xk((size_t)n_kf * 6), Tcw((size_t)n_kf * 12), Xp((size_t)n_pt * 3), Xl((size_t)n_ln * LD);
     for (size_t i = 0; i < xk.size(); ++i) xk[i] = st->kf_x[i];
     for (size_t i = 0; i < Tcw.size(); ++i) Tcw[i] = g->kf_Tcw[i];  // map poses (first linearisation)
     for (size_t i = 0; i < Xp.size(); ++i) Xp[i] = g->pt_xyz[i];
-    for (size_t i = 0; i < Xl.size(); ++i) Xl[i] = g->ln_orth[i];
+    for (size_t i = 0; i < Xl.size(); ++i) Xl[i] = gba ? st->ln_line3d[i] : g->ln_orth[i];
     std::vector<double> Lp((size_t)n_ln * 6);
-    for (size_t i = 0; i < Lp.size(); ++i) Lp[i] = st->ln_pluker[i];  // map NDw (first linearisation)
+    for (size_t i = 0; i < Lp.size() && !gba; ++i) Lp[i] = st->ln_pluker[i];  // map NDw (first linearisation)
     std::vector<Obs> obs((size_t)g->n_ept + g->n_eln);
     const double nobs = (double)(g->n_ept + g->n_eln);
 
@@ -373,8 +420,8 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
         err = 0.0;
         Hpp.assign((size_t)nf * 36, 0.0);
         gp.assign((size_t)nf * 6, 0.0);
-        Hll.assign((size_t)(n_pt + n_ln) * 16, 0.0);
-        gl.assign((size_t)(n_pt + n_ln) * 4, 0.0);
+        Hll.assign((size_t)(n_pt + n_ln) * 36, 0.0);
+        gl.assign((size_t)(n_pt + n_ln) * 6, 0.0);
         for (int e = 0; e < g->n_ept + g->n_eln; ++e) {
             Obs &s = obs[e];
             const bool pt = e < g->n_ept;
@@ -383,7 +430,7 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
             s.lm = pt ? g->ept_lm[ee] : n_pt + g->eln_lm[ee];
             s.kf = kf;
             s.h = hidx[kf];
-            std::fill(s.Jl, s.Jl + 4, 0.0);
+            std::fill(s.Jl, s.Jl + 6, 0.0);
             if (pt) {
                 // Tiw: map pose on the first linearisation and for KFs outside kf_list (:1657,1925)
                 double T[12];
@@ -391,6 +438,14 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
                 else std::memcpy(T, &Tcw[(size_t)kf * 12], sizeof T);
                 point_obs(T, &Xp[(size_t)g->ept_lm[ee] * 3], g->ept_obs + 2 * (size_t)ee, cam, p->homog_th, s.r, s.w,
                           s.Jp, s.Jl);
+            } else if (gba) {
+                // map pose (:3273, 3550); line3D on the first linearisation (:3270-3271), then
+                // Pwj = Qwj = X.block(6Nkf+3Npt+3·j) — the 6-dim blocks read at a stride of 3 (:3547-3548)
+                const int l = g->eln_lm[ee];
+                const double *P = first ? &Xl[(size_t)l * 6] : &Xl[(size_t)l * 3];
+                const double *Q = first ? &Xl[(size_t)l * 6 + 3] : &Xl[(size_t)l * 3];
+                gba_line_obs(g->kf_Tcw + (size_t)kf * 12, P, Q, g->eln_obs + 4 * (size_t)ee, cam, p->homog_th, s.r,
+                             s.w, s.Jp, s.Jl);
             } else {
                 // every line observation uses the map pose (:1750,2010); NDw from the map on the
                 // first linearisation, changeOrthToPluker(X) afterwards (:2003-2005)
@@ -401,12 +456,12 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
                 line_obs(g->kf_Tcw + (size_t)kf * 12, L, g->eln_obs + 4 * (size_t)ee, cam, p->homog_th, s.r, s.w, s.Jp,
                          s.Jl);
             }
-            const int D = pt ? 3 : 4;
+            const int D = pt ? 3 : LD;
             err += s.r * s.r * s.w;
-            double *H = &Hll[(size_t)s.lm * 16];
+            double *H = &Hll[(size_t)s.lm * 36];
             for (int i = 0; i < D; ++i) {
-                gl[(size_t)s.lm * 4 + i] += s.Jl[i] * s.r * s.w;
-                for (int j = 0; j < D; ++j) H[i * 4 + j] += s.Jl[i] * s.Jl[j] * s.w;
+                gl[(size_t)s.lm * 6 + i] += s.Jl[i] * s.r * s.w;
+                for (int j = 0; j < D; ++j) H[i * 6 + j] += s.Jl[i] * s.Jl[j] * s.w;
             }
             if (s.h >= 0) {
                 for (int i = 0; i < 6; ++i) {
@@ -423,15 +478,15 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
         for (int h = 0; h < nf; ++h)
             for (int i = 0; i < 6; ++i) m = std::max(m, std::fabs(Hpp[(size_t)h * 36 + i * 7]));
         for (int l = 0; l < n_pt + n_ln; ++l)
-            for (int i = 0; i < 4; ++i) m = std::max(m, std::fabs(Hll[(size_t)l * 16 + i * 5]));
+            for (int i = 0; i < 6; ++i) m = std::max(m, std::fabs(Hll[(size_t)l * 36 + i * 7]));
         return m;
     };
-    auto dim = [&](int l) { return l < n_pt ? 3 : 4; };
+    auto dim = [&](int l) { return l < n_pt ? 3 : LD; };
     // DX = (H + λ·diag H)⁻¹ g
     auto solve = [&]() -> bool {
         ++solves;
         std::fill(DX.begin(), DX.end(), 0.0);
-        auto col = [&](int l) { return 6 * nf + (l < n_pt ? 3 * l : 3 * n_pt + 4 * (l - n_pt)); };
+        auto col = [&](int l) { return 6 * nf + (l < n_pt ? 3 * l : 3 * n_pt + LD * (l - n_pt)); };
         if (o && o->dense) {  // the reference's dense H, literally
             std::vector<double> A((size_t)N * N, 0.0), b(N, 0.0);
             for (int h = 0; h < nf; ++h)
@@ -442,8 +497,8 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
             for (int l = 0; l < n_pt + n_ln; ++l) {
                 const int c0 = col(l), D = dim(l);
                 for (int i = 0; i < D; ++i) {
-                    b[c0 + i] = gl[(size_t)l * 4 + i];
-                    for (int j = 0; j < D; ++j) A[(size_t)(c0 + i) * N + c0 + j] = Hll[(size_t)l * 16 + i * 4 + j];
+                    b[c0 + i] = gl[(size_t)l * 6 + i];
+                    for (int j = 0; j < D; ++j) A[(size_t)(c0 + i) * N + c0 + j] = Hll[(size_t)l * 36 + i * 6 + j];
                 }
             }
             for (const Obs &s : obs) {
@@ -463,7 +518,7 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
         }
         // block elimination of the landmarks (exact; SimplicialLDLT differs by rounding only)
         const int nl = n_pt + n_ln, n = 6 * nf;
-        std::vector<double> Dinv((size_t)nl * 16, 0.0), S((size_t)n * n, 0.0), bs(n, 0.0);
+        std::vector<double> Dinv((size_t)nl * 36, 0.0), S((size_t)n * n, 0.0), bs(n, 0.0);
         for (int h = 0; h < nf; ++h)
             for (int i = 0; i < 6; ++i) {
                 bs[6 * h + i] = gp[(size_t)h * 6 + i];
@@ -475,11 +530,11 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
             for (int c = 0; c < D; ++c) {
                 std::vector<double> A(D * D), b(D, 0.0);
                 for (int i = 0; i < D; ++i)
-                    for (int j = 0; j < D; ++j) A[i * D + j] = Hll[(size_t)l * 16 + i * 4 + j];
+                    for (int j = 0; j < D; ++j) A[i * D + j] = Hll[(size_t)l * 36 + i * 6 + j];
                 for (int i = 0; i < D; ++i) A[i * D + i] += lambda * A[i * D + i];
                 b[c] = 1.0;
                 if (!ldlt_solve(A, D, b)) return false;
-                for (int i = 0; i < D; ++i) Dinv[(size_t)l * 16 + i * 4 + c] = b[i];
+                for (int i = 0; i < D; ++i) Dinv[(size_t)l * 36 + i * 6 + c] = b[i];
             }
         }
         // per landmark: its observations of free KFs, W_e = w Jpᵀ Jl (6 x D)
@@ -488,20 +543,20 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
             if (obs[e].h >= 0) lobs[obs[e].lm].push_back(e);
         for (int l = 0; l < nl; ++l) {
             const int D = dim(l);
-            const double *Di = &Dinv[(size_t)l * 16];
+            const double *Di = &Dinv[(size_t)l * 36];
             // y = D⁻¹ g_l
-            double y[4] = {0, 0, 0, 0};
+            double y[6] = {0, 0, 0, 0, 0, 0};
             for (int i = 0; i < D; ++i)
-                for (int j = 0; j < D; ++j) y[i] += Di[i * 4 + j] * gl[(size_t)l * 4 + j];
+                for (int j = 0; j < D; ++j) y[i] += Di[i * 6 + j] * gl[(size_t)l * 6 + j];
             for (int a : lobs[l]) {
                 const Obs &A = obs[a];
                 // b_s -= W_a y = Jp_a w_a (Jl_a · y)
                 double jy = 0;
                 for (int i = 0; i < D; ++i) jy += A.Jl[i] * y[i];
                 for (int i = 0; i < 6; ++i) bs[6 * A.h + i] -= A.Jp[i] * A.w * jy;
-                double zD[4] = {0, 0, 0, 0};  // Jl_a D⁻¹
+                double zD[6] = {0, 0, 0, 0, 0, 0};  // Jl_a D⁻¹
                 for (int j = 0; j < D; ++j)
-                    for (int i = 0; i < D; ++i) zD[j] += A.Jl[i] * Di[i * 4 + j];
+                    for (int i = 0; i < D; ++i) zD[j] += A.Jl[i] * Di[i * 6 + j];
                 for (int bb : lobs[l]) {
                     const Obs &B = obs[bb];
                     double s = 0;
@@ -517,18 +572,18 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
         for (int i = 0; i < n; ++i) DX[i] = xp[i];
         for (int l = 0; l < nl; ++l) {  // x_l = D⁻¹(g_l − Σ W_eᵀ x_p)
             const int D = dim(l);
-            double rr[4] = {0, 0, 0, 0};
-            for (int i = 0; i < D; ++i) rr[i] = gl[(size_t)l * 4 + i];
+            double rr[6] = {0, 0, 0, 0, 0, 0};
+            for (int i = 0; i < D; ++i) rr[i] = gl[(size_t)l * 6 + i];
             for (int a : lobs[l]) {
                 const Obs &A = obs[a];
                 double jx = 0;
                 for (int i = 0; i < 6; ++i) jx += A.Jp[i] * xp[6 * A.h + i];
                 for (int i = 0; i < D; ++i) rr[i] -= A.Jl[i] * A.w * jx;
             }
-            const double *Di = &Dinv[(size_t)l * 16];
+            const double *Di = &Dinv[(size_t)l * 36];
             for (int i = 0; i < D; ++i) {
                 double v = 0;
-                for (int j = 0; j < D; ++j) v += Di[i * 4 + j] * rr[j];
+                for (int j = 0; j < D; ++j) v += Di[i * 6 + j] * rr[j];
                 DX[col(l) + i] = v;
             }
         }
@@ -548,6 +603,10 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
         }
         for (int i = 0; i < 3 * n_pt; ++i) Xp[i] += DX[6 * nf + i];
         for (int l = 0; l < n_ln; ++l) {
+            if (gba) {  // GBA: X += DX for every landmark (:3690-3691)
+                for (int i = 0; i < 6; ++i) Xl[(size_t)l * 6 + i] += DX[6 * nf + 3 * n_pt + 6 * l + i];
+                continue;
+            }
             double out[4];
             update_orth(&Xl[(size_t)l * 4], &DX[6 * nf + 3 * n_pt + 4 * l], out);
             for (int i = 0; i < 4; ++i) Xl[(size_t)l * 4 + i] = out[i];
@@ -569,7 +628,9 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
     // first iteration (:1639-1895)
     if (N > 0 && !obs.empty()) {
         linearize(true);
-        lambda *= hmax();
+        // GBA keeps Hmax in an int (:3386): the maximum truncated toward zero (|H_ii| >= 2^31 would
+        // be an undefined conversion in the reference; it is taken as a 64-bit truncation here)
+        lambda *= gba ? (double)(long long)hmax() : hmax();
         const double l0 = lambda;
         if (solve()) apply();
         dxn = dxnorm();
@@ -606,7 +667,8 @@ int refhlm_lba(const plba_graph *g, const plba_hlm_state *st, const plba_hlm_par
                 std::memcpy(res->kf_Tcw + (size_t)k * 12, hidx[k] >= 0 ? &Tcw[(size_t)k * 12] : g->kf_Tcw + (size_t)k * 12,
                             12 * sizeof(double));
         if (res->pt_xyz) std::memcpy(res->pt_xyz, Xp.data(), Xp.size() * sizeof(double));
-        if (res->ln_orth) std::memcpy(res->ln_orth, Xl.data(), Xl.size() * sizeof(double));
+        if (res->ln_orth && !gba) std::memcpy(res->ln_orth, Xl.data(), Xl.size() * sizeof(double));
+        if (res->ln_line3d && gba) std::memcpy(res->ln_line3d, Xl.data(), Xl.size() * sizeof(double));
         res->linearizations = lin;
         res->solves = solves;
         res->accepted = acc;
@@ -626,6 +688,10 @@ void refhlm_point_obs(const double *Tcw, const double *xyz, const double *obs, d
 void refhlm_line_obs(const double *Tcw, const double *pluker, const double *obs, double fx, double fy, double cx,
                      double cy, double homog_th, double *r, double *w, double *Jp, double *Jl) {
     line_obs(Tcw, pluker, obs, Cam{fx, fy, cx, cy}, homog_th, *r, *w, Jp, Jl);
+}
+void refhlm_gba_line_obs(const double *Tcw, const double *P, const double *Q, const double *lo, double fx, double fy,
+                         double cx, double cy, double homog_th, double *r, double *w, double *Jp, double *Jl) {
+    gba_line_obs(Tcw, P, Q, lo, Cam{fx, fy, cx, cy}, homog_th, *r, *w, Jp, Jl);
 }
 void refhlm_expmap(const double *x, double *T) { expmap(x, T); }
 void refhlm_logmap(const double *T, double *x) { logmap(T, x); }

@@ -818,6 +818,14 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.Xb[1], X.size());
     ALLOC(d.xk[0], (size_t)n_kf * 6);
     ALLOC(d.xk[1], (size_t)n_kf * 6);
+    // hand-rolled GBA: endpoint lines in the reference's (global) order, their 6x6 blocks
+    ALLOC(d.XL[0], (size_t)std::max(n_ln_g, 1) * 6);
+    ALLOC(d.XL[1], (size_t)std::max(n_ln_g, 1) * 6);
+    ALLOC(d.Hl6, (size_t)std::max(n_ln, 1) * 21);
+    ALLOC(d.bl6, (size_t)std::max(n_ln, 1) * 6);
+    std::vector<int32_t> ln_gidx(std::max(n_ln, 1), 0);
+    for (int i = 0; i < n_ln; ++i) ln_gidx[i] = lm_gpos[n_pt + i] - n_pt_g;
+    UPLOAD(d.ln_gidx, ln_gidx);
     ALLOC(d.Lpb[0], (size_t)std::max(n_ln, 1) * 8);
     ALLOC(d.Lpb[1], (size_t)std::max(n_ln, 1) * 8);
     UPLOAD(d.kf_hidx, kf_hidx);
@@ -1487,6 +1495,8 @@ void plba_hlm_default_params(plba_hlm_params *p) {
     p->min_error_change = 1e-7; // :85
     p->max_iters = 15;          // src/slamConfig.cpp:67
     p->err_per_obs = 0;
+    p->variant = PLBA_HLM_LBA_PLUCKER;
+    p->pad = 0;
 }
 
 // MapHandler::levMarquardtOptimizationLBAForPluker (src/mapHandler.cpp:1618-2332) on the uploaded
@@ -1499,9 +1509,18 @@ int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params 
     plba_hlm_params prm;
     if (p) prm = *p;
     else plba_hlm_default_params(&prm);
-    if (prm.max_iters < 1) {
-        ctx->set_error("max_iters must be >= 1");
+    if (prm.max_iters < 1 || (prm.variant != PLBA_HLM_LBA_PLUCKER && prm.variant != PLBA_HLM_GBA)) {
+        ctx->set_error("max_iters must be >= 1 and variant PLBA_HLM_LBA_PLUCKER or PLBA_HLM_GBA");
         return PLBA_E_INVALID;
+    }
+    const bool gba = prm.variant == PLBA_HLM_GBA;
+    if (gba && ctx->n_ln && !st->ln_line3d) {
+        ctx->set_error("the GBA variant needs state ln_line3d");
+        return PLBA_E_INVALID;
+    }
+    if (gba && ctx->d.sharded) {
+        ctx->set_error("the GBA variant runs on unsharded windows only");
+        return PLBA_E_STATE;
     }
     int rc = plba_reset_estimates(ctx);
     if (rc) return rc;
@@ -1509,18 +1528,22 @@ int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params 
     ctx->trace.clear();
     // X_aux pose blocks and the map's NDw (in this rank's device landmark order)
     std::vector<double> Lm((size_t)std::max(d.n_ln, 1) * 8, 0.0);
-    for (int i = 0; i < d.n_ln; ++i) {
+    for (int i = 0; i < d.n_ln && !gba; ++i) {
         const int gl = ctx->lm_gpos[d.n_pt + i] - ctx->n_pt;
         for (int k = 0; k < 6; ++k) Lm[(size_t)i * 8 + k] = st->ln_pluker[(size_t)gl * 6 + k];
     }
     if (d.n_kf) PLBA_CHECK(hipMemcpyAsync(d.xk[0], st->kf_x, sizeof(double) * (size_t)d.n_kf * 6, hipMemcpyHostToDevice, ctx->stream));
-    if (d.n_ln) PLBA_CHECK(hipMemcpyAsync(d.Lpb[0], Lm.data(), sizeof(double) * Lm.size(), hipMemcpyHostToDevice, ctx->stream));
+    if (d.n_ln && !gba)
+        PLBA_CHECK(hipMemcpyAsync(d.Lpb[0], Lm.data(), sizeof(double) * Lm.size(), hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->n_ln && gba)
+        PLBA_CHECK(hipMemcpyAsync(d.XL[0], st->ln_line3d, sizeof(double) * (size_t)ctx->n_ln * 6, hipMemcpyHostToDevice,
+                                  ctx->stream));
     auto t0 = std::chrono::steady_clock::now();
     Ctrl c = schedule_init(ctx, 1);
     c.max_iters[0] = prm.max_iters;
     c.stage_robust[0] = 0;
     c.stage_level[0] = 0;
-    c.hlm = 1;
+    c.hlm = gba ? 2 : 1;
     c.hlm_lambda0 = prm.lambda0;
     c.hlm_k = prm.lambda_k;
     c.hlm_homog = prm.homog_th;
@@ -1550,7 +1573,9 @@ int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params 
         PLBA_CHECK(hipMemcpy(res->kf_x, d.xk[ctx->cur], sizeof(double) * (size_t)d.n_kf * 6, hipMemcpyDeviceToHost));
         // KFs outside kf_list keep the caller's x (the device copy carries them through unchanged)
     }
-    return plba_download(ctx, res->kf_Tcw, res->pt_xyz, res->ln_orth);
+    if (gba && res->ln_line3d && ctx->n_ln)
+        PLBA_CHECK(hipMemcpy(res->ln_line3d, d.XL[ctx->cur], sizeof(double) * (size_t)ctx->n_ln * 6, hipMemcpyDeviceToHost));
+    return plba_download(ctx, res->kf_Tcw, res->pt_xyz, gba ? nullptr : res->ln_orth);
 }
 
 int plba_get_trace(plba_ctx *ctx, plba_iter_trace *out, int32_t cap, int32_t *n) {

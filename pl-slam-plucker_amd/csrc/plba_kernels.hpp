@@ -87,6 +87,9 @@ struct Dev {
     double *Tb[2], *T_init;             // [n_kf][12]
     double *Xb[2], *X_init;             // [n_lm][4]
     double *xk[2];                      // [n_kf][6] se(3) pose vectors X_i of the hand-rolled LM
+    double *XL[2];                      // [n_ln_g][6] GBA line3D endpoints, reference (global) line order
+    double *Hl6, *bl6;                  // [n_ln][21], [n_ln][6] GBA line blocks (packed lower 6x6)
+    int32_t *ln_gidx;                   // [n_ln] device line -> reference (global) line index
     double *Lpb[2];                     // [n_ln][8]: Plücker vector (6) of each line at Xb[i]
                                         //   (k_line_pluker at schedule start, then k_lm_solve)
     int32_t *kf_hidx;                   // [n_kf]
@@ -314,8 +317,18 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
             const int lm = d.e_lm[e], kf = d.e_kf[e];
             const double *obs = d.e_obs + (size_t)e * 4;
             double r, w, Jp[6], Jl[4];
+            double Jl6[6] = {0, 0, 0, 0, 0, 0};
             if (e < d.Ep) {
                 hlm_point(Tcur(d) + (size_t)kf * 12, Xcur(d) + (size_t)lm * 4, obs, d.cam, cc->hlm_homog, r, w, Jp, Jl);
+            } else if (cc->hlm == 2) {
+                // GBA: map pose, endpoints line3D on the first linearisation, then both read from
+                // the aliased X.block(6Nkf+3Npt+3·j) (src/mapHandler.cpp:3547-3548)
+                const int j = d.ln_gidx[lm - d.n_pt];
+                const double *XLc = d.XL[cc->cur];
+                const bool first = cc->iter == 0;
+                const double *P = XLc + (first ? (size_t)j * 6 : (size_t)j * 3);
+                const double *Q = XLc + (first ? (size_t)j * 6 + 3 : (size_t)j * 3);
+                gba_line(d.T_init + (size_t)kf * 12, P, Q, obs, d.cam, cc->hlm_homog, r, w, Jp, Jl6);
             } else {
                 const double *Lc = d.Lpb[cc->cur] + (size_t)(lm - d.n_pt) * 8;
                 double L[6];
@@ -334,10 +347,16 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
             }
             c[0] = sw * r;
             c[1] = 0.0;
+            if (e >= d.Ep && cc->hlm == 2) {  // 6-dim landmark row, flat in B
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                B[k] = sw * Jl[k];
-                B[4 + k] = 0.0;
+                for (int k = 0; k < 6; ++k) B[k] = sw * Jl6[k];
+                B[6] = B[7] = 0.0;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    B[k] = sw * Jl[k];
+                    B[4 + k] = 0.0;
+                }
             }
         } else if (d.e_active[e]) {
             const int lm = d.e_lm[e], kf = d.e_kf[e];
@@ -461,6 +480,32 @@ __device__ __forceinline__ void landmark_reduce(const Dev &d, int lb) {
             d.lm_active[l] = act ? 1 : 0;
         }
         any = d.lm_active[l] != 0;
+        if (l >= d.n_pt && d.ctrl->hlm == 2) {  // GBA line: 6x6 block (flat 6-vector rows in B)
+            double H6[21], b6[6];
+#pragma unroll
+            for (int k = 0; k < 21; ++k) H6[k] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) b6[k] = 0.0;
+            for (int e = d.lm_off[l]; e < d.lm_off[l + 1]; ++e) {
+                double bb[6];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) bb[k] = d.B[(size_t)e * 8 + k];
+                const double c0 = d.cvec[(size_t)e * 2];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+#pragma unroll
+                    for (int cc = 0; cc <= r; ++cc) H6[pk(r, cc)] += bb[r] * bb[cc];
+                    b6[r] += bb[r] * c0;
+                }
+            }
+            const int li = l - d.n_pt;
+#pragma unroll
+            for (int k = 0; k < 21; ++k) d.Hl6[(size_t)li * 21 + k] = H6[k];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) d.bl6[(size_t)li * 6 + k] = b6[k];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(H6[pk(k, k)]));
+        } else {
         double H[10], b[4];
 #pragma unroll
         for (int k = 0; k < 10; ++k) H[k] = 0.0;
@@ -494,6 +539,7 @@ __device__ __forceinline__ void landmark_reduce(const Dev &d, int lb) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.bl[(size_t)l * 4 + k] = b[k];
         mx = fmax(fmax(fabs(H[pk(0, 0)]), fabs(H[pk(1, 1)])), fmax(fabs(H[pk(2, 2)]), fabs(H[pk(3, 3)])));
+        }
     }
     double m = block_max<kLmBlock>(mx, sh);
     const int anyb = __syncthreads_or(any ? 1 : 0);
@@ -606,7 +652,8 @@ __global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
             c->hlm_lin += 1;
             if (c->iter == 0) {
                 c->maxdiag = mx;
-                c->lambda = c->hlm_lambda0 * mx;
+                // GBA keeps Hmax in an int (src/mapHandler.cpp:3386): truncated toward zero
+                c->lambda = c->hlm_lambda0 * (c->hlm == 2 ? (double)(long long)mx : mx);
             } else if (fabs(err - c->err_prev) < c->hlm_minchg || err < c->hlm_minerr) {
                 if (c->ntrace < kTraceCap)
                     d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, 0, 3, err, err, c->lambda, c->lambda};
@@ -688,6 +735,7 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
     const int full = nb - 8 * (per - 1);  // XCDs that get `per` chunks (the rest get per-1)
     const int ch = xcd < full ? xcd * per + slot : full * per + (xcd - full) * (per - 1) + slot;
     const int lane = threadIdx.x;
+    const bool hlm = d.ctrl->hlm != 0;
     const int b = d.ch_blk[ch];
     const bool diag = d.blk_i1[b] == d.blk_i2[b];
     double acc[42];
@@ -714,6 +762,9 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
                 m10 = fma(z1[4 + k], z2[k], m10);
                 m11 = fma(z1[4 + k], z2[4 + k], m11);
             }
+            // hand-rolled LM: A has one live row, so only m00 is used — and a GBA line's Z_e
+            // (6 entries) spills into Z's second row: the full 8-entry product
+            if (hlm) m00 += m11;
             double Q[12];
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
@@ -1673,6 +1724,50 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
     const int e = blockIdx.x * kBlock + threadIdx.x;
     if (e >= d.E) return;
     const int l = d.e_lm[e];
+    if (e >= d.Ep && d.ctrl->hlm == 2) {  // GBA line: 6x6 (Hl6 + λ·diag) = L Lᵀ, Z_e = L⁻¹ b_e, q_e = Z_e·L⁻¹ b_l
+        const double lam = d.ctrl->lambda;
+        const int li = l - d.n_pt;
+        double H[21], L6[21], g6[6], bb[6], z[6];
+#pragma unroll
+        for (int k = 0; k < 21; ++k) { H[k] = d.Hl6[(size_t)li * 21 + k]; L6[k] = 0.0; }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double sj = H[pk(j, j)] + lam * H[pk(j, j)];
+#pragma unroll
+            for (int p = 0; p < j; ++p) sj -= L6[pk(j, p)] * L6[pk(j, p)];
+            const double djj = sqrt(sj);
+            L6[pk(j, j)] = djj;
+#pragma unroll
+            for (int i = j + 1; i < 6; ++i) {
+                double t = H[pk(i, j)];
+#pragma unroll
+                for (int p = 0; p < j; ++p) t -= L6[pk(i, p)] * L6[pk(j, p)];
+                L6[pk(i, j)] = t / djj;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) bb[k] = d.B[(size_t)e * 8 + k];
+        double q0 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double t = bb[i], tg = d.bl6[(size_t)li * 6 + i];
+#pragma unroll
+            for (int p = 0; p < i; ++p) {
+                t -= L6[pk(i, p)] * z[p];
+                tg -= L6[pk(i, p)] * g6[p];
+            }
+            z[i] = t / L6[pk(i, i)];
+            g6[i] = tg / L6[pk(i, i)];
+            q0 += z[i] * g6[i];
+        }
+        double *Z = d.Z + (size_t)e * 8;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Z[k] = z[k];
+        Z[6] = Z[7] = 0.0;
+        d.q[(size_t)e * 2 + 0] = q0;
+        d.q[(size_t)e * 2 + 1] = 0.0;
+        return;
+    }
     const int DIM = e < d.Ep ? 3 : 4;
     double L[10], g[4], B[8];
     lm_chol(d, l, d.ctrl->lambda, d.ctrl->hlm != 0, L, g);
@@ -1799,8 +1894,10 @@ __device__ __forceinline__ void lm_load_edge(const Dev &d, int e, LmEdge &s) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) s.B[k] = d.B[(size_t)e * 8 + k];
 }
-// u += B_eᵀ (A_e x_p) for an edge of a free pose
-__device__ __forceinline__ void lm_hpl_x(const LmEdge &s, const double (&x)[6], double (&u)[4]) {
+// u += B_eᵀ (A_e x_p) for an edge of a free pose; a GBA line's 6-entry row (flat in B, A's second
+// row zero) also feeds u45 (components 4, 5)
+template <bool GBA = false>
+__device__ __forceinline__ void lm_hpl_x(const LmEdge &s, const double (&x)[6], double (&u)[4], double (&u45)[2]) {
     double ax0 = 0, ax1 = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -1809,6 +1906,10 @@ __device__ __forceinline__ void lm_hpl_x(const LmEdge &s, const double (&x)[6], 
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] += s.B[i] * ax0 + s.B[4 + i] * ax1;
+    if (GBA) {
+        u45[0] += s.B[4] * ax0;
+        u45[1] += s.B[5] * ax0;
+    }
 }
 // robust χ² of one active edge at the trial state (computeActiveErrors)
 __device__ __forceinline__ double lm_eval(const Dev &d, const LmEdge &s, const double *T, bool pt, const double (&X)[4],
@@ -1989,11 +2090,18 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
     }
     double chi = 0.0, sc = 0.0;
     // r = b_l − Σ_e Hpl_eᵀ x_p,  Hpl_eᵀ x_p = B_eᵀ (A_e x_p)  (edges of a fixed pose: 0)
-    double u[4] = {0, 0, 0, 0};
+    double u[4] = {0, 0, 0, 0}, u45[2] = {0, 0};
+    const bool gba_ln = cg->hlm == 2 && live && !is_point_lm(d, l);  // uniform across the quad
     if (act && solve && !(d.diag & 4)) {
+        if (gba_ln) {
 #pragma unroll
-        for (int j = 0; j < kLmSlots; ++j)
-            if (sv[j] && sl[j].h >= 0) lm_hpl_x(sl[j], xs[j], u);
+            for (int j = 0; j < kLmSlots; ++j)
+                if (sv[j] && sl[j].h >= 0) lm_hpl_x<true>(sl[j], xs[j], u, u45);
+        } else {
+#pragma unroll
+            for (int j = 0; j < kLmSlots; ++j)
+                if (sv[j] && sl[j].h >= 0) lm_hpl_x(sl[j], xs[j], u, u45);
+        }
         for (int e = off0 + q + kLmLanes * kLmSlots; e < off1; e += kLmLanes) {  // long tracks
             LmEdge s;
             lm_load_edge(d, e, s);
@@ -2001,12 +2109,72 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
             double x[6];
 #pragma unroll
             for (int k = 0; k < 6; ++k) x[k] = d.xp[6 * s.h + k];
-            lm_hpl_x(s, x, u);
+            if (gba_ln) lm_hpl_x<true>(s, x, u, u45);
+            else lm_hpl_x(s, x, u, u45);
         }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = quad_sum(u[i]);  // all lanes: DPP reads the whole quad
-    if (live) {
+    if (cg->hlm == 2) {
+        u45[0] = quad_sum(u45[0]);
+        u45[1] = quad_sum(u45[1]);
+    }
+    if (live && gba_ln) {
+        // GBA line (src/mapHandler.cpp:3673-3691): x = (Hl6 + λ·diag)⁻¹ (b_l − Σ_e b_e a_e·x_p),
+        // X += DX on the 6 endpoint coordinates, ‖DX‖² partial; lane q == 0 writes
+        const int li = l - d.n_pt, j = d.ln_gidx[li];
+        const double *XLc = d.XL[cur] + (size_t)j * 6;
+        double *XLt = d.XL[cur ^ 1] + (size_t)j * 6;
+        double *Xt = d.Xb[cur ^ 1] + (size_t)l * 4;
+        if (act && solve) {
+            double H[21], L6[21], y[6], x[6];
+#pragma unroll
+            for (int k = 0; k < 21; ++k) { H[k] = d.Hl6[(size_t)li * 21 + k]; L6[k] = 0.0; }
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) {
+                double sj = H[pk(jj, jj)] + lam * H[pk(jj, jj)];
+#pragma unroll
+                for (int p = 0; p < jj; ++p) sj -= L6[pk(jj, p)] * L6[pk(jj, p)];
+                const double djj = sqrt(sj);
+                L6[pk(jj, jj)] = djj;
+#pragma unroll
+                for (int i = jj + 1; i < 6; ++i) {
+                    double t = H[pk(i, jj)];
+#pragma unroll
+                    for (int p = 0; p < jj; ++p) t -= L6[pk(i, p)] * L6[pk(jj, p)];
+                    L6[pk(i, jj)] = t / djj;
+                }
+            }
+            const double uu[6] = {u[0], u[1], u[2], u[3], u45[0], u45[1]};
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double t = d.bl6[(size_t)li * 6 + i] - uu[i];
+#pragma unroll
+                for (int p = 0; p < i; ++p) t -= L6[pk(i, p)] * y[p];
+                y[i] = t / L6[pk(i, i)];
+            }
+#pragma unroll
+            for (int i = 5; i >= 0; --i) {
+                double t = y[i];
+#pragma unroll
+                for (int p = i + 1; p < 6; ++p) t -= L6[pk(p, i)] * x[p];
+                x[i] = t / L6[pk(i, i)];
+            }
+            if (q == 0) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    sc += x[i] * x[i];
+                    XLt[i] = XLc[i] + x[i];
+                }
+            }
+        } else if (q == 0) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) XLt[i] = XLc[i];
+        }
+        if (q == 0)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
+    } else if (live) {
         double *Xt = d.Xb[cur ^ 1] + (size_t)l * 4;
         if (act) {
             const bool pt = is_point_lm(d, l);

@@ -502,4 +502,43 @@ PLBA_HD void hlm_line(const double *T, const double *L, const double *obs, const
     w = 1.0 / (1.0 + r * r);
 }
 
+// One GBA line observation (MapHandler::levMarquardtOptimizationGBA, src/mapHandler.cpp:3270-3340 /
+// :3545-3619): endpoints P, Q in the world, image line lo = (a, b, c); e = (lo·π(P), lo·π(Q));
+// the rows use fx·e0 / fy·e1 (lx = l_err(0), ly = l_err(1), :3293-3296); Jl = [J_P·e0; J_Q·e1]/m.
+PLBA_HD void gba_line(const double *T, const double *P, const double *Q, const double *lo, const Cam &c, double hth,
+                      double &r, double &w, double *Jp, double *Jl) {
+    double Pi[3], Qi[3];
+    point_pc(T, P, Pi);
+    point_pc(T, Q, Qi);
+    const double pu = c.cx + c.fx * Pi[0] / Pi[2], pv = c.cy + c.fy * Pi[1] / Pi[2];
+    const double qu = c.cx + c.fx * Qi[0] / Qi[2], qv = c.cy + c.fy * Qi[1] / Qi[2];
+    const double e0 = lo[0] * pu + lo[1] * pv + lo[2];
+    const double e1 = lo[0] * qu + lo[1] * qv + lo[2];
+    r = sqrt(e0 * e0 + e1 * e1);
+    const double fxlx = c.fx * e0, fyly = c.fy * e1;
+    const double m = fmax(hth, r);
+    double JPi[6], JQi[6];
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        const double *G = side ? Qi : Pi;
+        double *Jpose = side ? JQi : JPi;
+        const double ek = side ? e1 : e0;
+        const double gx = G[0], gy = G[1], gz = G[2];
+        const double gz2 = 1.0 / fmax(hth, gz * gz);
+        Jpose[0] = gz2 * fxlx * gz;
+        Jpose[1] = gz2 * fyly * gz;
+        Jpose[2] = -gz2 * (fxlx * gx + fyly * gy);
+        Jpose[3] = -gz2 * (fxlx * gx * gy + fyly * gy * gy + fyly * gz * gz);
+        Jpose[4] = gz2 * (fxlx * gx * gx + fxlx * gz * gz + fyly * gx * gy);
+        Jpose[5] = gz2 * (fyly * gx * gz - fxlx * gy * gz);
+        const double j0 = gz2 * fxlx * gz, j1 = gz2 * fyly * gz, j2 = -gz2 * (fxlx * gx + fyly * gy);
+        Jl[3 * side + 0] = ((j0 * T[0] + j1 * T[4] + j2 * T[8]) * ek) / m;
+        Jl[3 * side + 1] = ((j0 * T[1] + j1 * T[5] + j2 * T[9]) * ek) / m;
+        Jl[3 * side + 2] = ((j0 * T[2] + j1 * T[6] + j2 * T[10]) * ek) / m;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Jp[k] = (JPi[k] * e0 + JQi[k] * e1) / m;
+    w = 1.0 / (1.0 + r * r);
+}
+
 }  // namespace plba

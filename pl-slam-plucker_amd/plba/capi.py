@@ -133,35 +133,52 @@ def trace_to_array(tr, n: int) -> np.ndarray:
 
 # ---- hand-rolled LM (plba_hlm_*)
 class PlbaHlmState(C.Structure):
-    _fields_ = [("kf_x", _dp), ("ln_pluker", _dp)]
+    _fields_ = [("kf_x", _dp), ("ln_pluker", _dp), ("ln_line3d", _dp)]
 
 
 class PlbaHlmParams(C.Structure):
     _fields_ = [("lambda0", C.c_double), ("lambda_k", C.c_double), ("homog_th", C.c_double),
                 ("min_error", C.c_double), ("min_error_change", C.c_double),
-                ("max_iters", C.c_int32), ("err_per_obs", C.c_int32)]
+                ("max_iters", C.c_int32), ("err_per_obs", C.c_int32), ("variant", C.c_int32), ("pad", C.c_int32)]
+
+
+HLM_LBA_PLUCKER = 0
+HLM_GBA = 1
+DBL_EPSILON = float(np.finfo(np.float64).eps)
 
 
 class PlbaHlmResult(C.Structure):
     _fields_ = [("kf_x", _dp), ("kf_Tcw", _dp), ("pt_xyz", _dp), ("ln_orth", _dp),
                 ("linearizations", C.c_int32), ("solves", C.c_int32), ("accepted", C.c_int32), ("pad", C.c_int32),
-                ("err", C.c_double), ("lambda_", C.c_double), ("dx_norm", C.c_double), ("solve_ms", C.c_double)]
+                ("err", C.c_double), ("lambda_", C.c_double), ("dx_norm", C.c_double), ("solve_ms", C.c_double),
+                ("ln_line3d", _dp)]
+
+
+def gba_params(**kw) -> "PlbaHlmParams":
+    """levMarquardtOptimizationGBA: the LBA defaults with ε stop tests (src/mapHandler.cpp:3664,3694)."""
+    p = hlm_params(min_error=DBL_EPSILON, min_error_change=DBL_EPSILON, variant=HLM_GBA)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
 
 
 def hlm_params(**kw) -> PlbaHlmParams:
     """Defaults of src/slamConfig.cpp:65-67 and src2/config.cpp:80-85 (plba_hlm_default_params)."""
     p = PlbaHlmParams(lambda0=1e-5, lambda_k=10.0, homog_th=1e-7, min_error=1e-7, min_error_change=1e-7,
-                      max_iters=15, err_per_obs=0)
+                      max_iters=15, err_per_obs=0, variant=HLM_LBA_PLUCKER)
     for k, v in kw.items():
         setattr(p, k, v)
     return p
 
 
 class HlmStateView:
-    def __init__(self, kf_x: np.ndarray, ln_pluker: np.ndarray):
+    def __init__(self, kf_x: np.ndarray, ln_pluker: np.ndarray, ln_line3d=None):
         self.kf_x = np.ascontiguousarray(kf_x, np.float64).reshape(-1, 6)
         self.ln_pluker = np.ascontiguousarray(ln_pluker, np.float64).reshape(-1, 6)
-        self.struct = PlbaHlmState(kf_x=_ptr(self.kf_x, _dp), ln_pluker=_ptr(self.ln_pluker, _dp))
+        self.ln_line3d = np.ascontiguousarray(ln_line3d if ln_line3d is not None else np.zeros((0, 6)),
+                                              np.float64).reshape(-1, 6)
+        self.struct = PlbaHlmState(kf_x=_ptr(self.kf_x, _dp), ln_pluker=_ptr(self.ln_pluker, _dp),
+                                   ln_line3d=_ptr(self.ln_line3d, _dp) if self.ln_line3d.size else None)
 
 
 class HlmResultBuffers:
@@ -170,11 +187,14 @@ class HlmResultBuffers:
         self.kf_Tcw = np.zeros((g.n_kf, 3, 4))
         self.pt_xyz = np.zeros((g.n_pt, 3))
         self.ln_orth = np.zeros((g.n_ln, 4))
+        self.ln_line3d = np.zeros((g.n_ln, 6))
         self.struct = PlbaHlmResult(kf_x=_ptr(self.kf_x, _dp), kf_Tcw=_ptr(self.kf_Tcw, _dp),
-                                    pt_xyz=_ptr(self.pt_xyz, _dp), ln_orth=_ptr(self.ln_orth, _dp))
+                                    pt_xyz=_ptr(self.pt_xyz, _dp), ln_orth=_ptr(self.ln_orth, _dp),
+                                    ln_line3d=_ptr(self.ln_line3d, _dp))
 
     def as_dict(self) -> dict:
         s = self.struct
         return dict(kf_x=self.kf_x, kf_Tcw=self.kf_Tcw, pt_xyz=self.pt_xyz, ln_orth=self.ln_orth,
+                    ln_line3d=self.ln_line3d,
                     linearizations=int(s.linearizations), solves=int(s.solves), accepted=int(s.accepted),
                     err=float(s.err), lam=float(s.lambda_), dx_norm=float(s.dx_norm), solve_ms=float(s.solve_ms))

@@ -242,7 +242,7 @@ class Solver:
         if params is None:
             params = capi.PlbaHlmParams()
             self.L.plba_hlm_default_params(C.byref(params))
-        sv = capi.HlmStateView(win.kf_x, win.ln_pluker)
+        sv = capi.HlmStateView(win.kf_x, win.ln_pluker, getattr(win, "ln_line3d", None))
         rb = capi.HlmResultBuffers(g)
         self._check(self.L.plba_hlm_lba(self.ctx, C.byref(sv.struct), C.byref(params), C.byref(rb.struct)),
                     "plba_hlm_lba")

@@ -88,6 +88,9 @@ class Graph:
     gt_orth: Optional[np.ndarray] = None
     ept_outlier: Optional[np.ndarray] = None
     eln_outlier: Optional[np.ndarray] = None
+    # initial line endpoints [P; Q] (N_l,6): the non-Plücker map's line3D, read by the hand-rolled
+    # GBA (src/mapHandler.cpp:3089); not an input of the Plücker LBA
+    ln_seg0: Optional[np.ndarray] = None
 
     @property
     def n_kf(self) -> int:
@@ -318,6 +321,7 @@ def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int
         xyz0 = gt_xyz + rng.normal(0.0, 0.03, gt_xyz.shape)
         orth0 = gt_orth + rng.normal(0.0, math.radians(0.3), gt_orth.shape)
     Tcw0 = geo.invert_rigid(np.concatenate([Rwc0, pwc0[..., None]], -1))
+    seg0 = seg.reshape(-1, 6) + (rng.normal(0.0, 0.03, (n_ln, 6)) if perturb else 0.0)
     # the map stores NDw; the LBA converts it to orth (src/mapHandler.cpp:6039-6040)
     ln_orth = geo.pluker_to_orth(geo.orth_to_pluker(orth0)) if n_ln else orth0
 
@@ -337,6 +341,7 @@ def generate(name: str = "C3", *, n_kf: Optional[int] = None, n_pt: Optional[int
         eln_lm=eln_lm, eln_kf=eln_kf, eln_obs=np.ascontiguousarray(eln_obs), eln_info=np.full(E_l, info),
         gt_Tcw=gt_Tcw, gt_xyz=gt_xyz, gt_orth=gt_orth,
         ept_outlier=ept_outlier.astype(np.uint8), eln_outlier=eln_outlier.astype(np.uint8),
+        ln_seg0=np.ascontiguousarray(seg0),
     )
 
 

@@ -148,6 +148,7 @@ def _hlm_lib():
         L.refhlm_lba.restype = C.c_int
         L.refhlm_point_obs.argtypes = [dp, dp, dp] + [C.c_double] * 5 + [dp, dp, dp, dp]
         L.refhlm_line_obs.argtypes = [dp, dp, dp] + [C.c_double] * 5 + [dp, dp, dp, dp]
+        L.refhlm_gba_line_obs.argtypes = [dp, dp, dp, dp] + [C.c_double] * 5 + [dp, dp, dp, dp]
         L.refhlm_expmap.argtypes = [dp, dp]
         L.refhlm_logmap.argtypes = [dp, dp]
         L.refhlm_inverse_se3.argtypes = [dp, dp]
@@ -159,7 +160,7 @@ def hlm_lba(win, params=None, dense: bool = False) -> dict:
     """levMarquardtOptimizationLBAForPluker on an HlmWindow (plba.hlm.hlm_window)."""
     g = win.graph
     gv = capi.GraphView(g)
-    sv = capi.HlmStateView(win.kf_x, win.ln_pluker)
+    sv = capi.HlmStateView(win.kf_x, win.ln_pluker, getattr(win, "ln_line3d", None))
     rb = capi.HlmResultBuffers(g)
     cap = 64
     tr = (capi.PlbaIterTrace * cap)()
@@ -201,3 +202,10 @@ def hlm_logmap(T):
     x = np.zeros(6)
     _hlm_lib().refhlm_logmap(_p(T), _p(x))
     return x
+
+
+def gba_line_obs(Tcw, P, Q, lo, cam, homog_th=1e-7):
+    a = [np.ascontiguousarray(v, np.float64).reshape(-1) for v in (Tcw, P, Q, lo)]
+    r, w, Jp, Jl = np.zeros(1), np.zeros(1), np.zeros(6), np.zeros(6)
+    _hlm_lib().refhlm_gba_line_obs(*[_p(v) for v in a], *cam, homog_th, _p(r), _p(w), _p(Jp), _p(Jl))
+    return r[0], w[0], Jp, Jl

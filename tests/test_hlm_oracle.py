@@ -10,7 +10,9 @@ checks pin the restatement instead:
   * the line observation's rows against a literal numpy transcription of the reference's Eigen
     expressions (:1744-1811 — fai_e carries fenmu factors, so these are not derivatives);
   * the exact block (Schur) solve against the reference's literal dense N×N H + LDLᵀ;
-  * the reference's control flow: err /= 0 → +inf, every step applied, λ ×10 per step.
+  * the reference's control flow: err /= 0 → +inf, every step applied, λ ×10 per step;
+  * levMarquardtOptimizationGBA (:3128-3726): its endpoint-line rows against a literal numpy
+    transcription, and its block solve (6-dim line blocks) against the literal dense H.
 """
 import numpy as np
 import pytest
@@ -174,3 +176,57 @@ def test_per_observation_divisor_stops_on_small_change():
     tr = out["trace"]
     assert tr["result"][-1] in (0, 1, 3)
     assert out["linearizations"] == out["solves"] + (1 if tr["result"][-1] == 3 else 0)
+
+
+def _gba_line_literal(Tcw, P, Q, lo, cam, hth=1e-7):
+    """src/mapHandler.cpp:3270-3340 transcribed with numpy (lx, ly are the two residuals)."""
+    fx, fy, cx, cy = cam
+    R, t = Tcw[:, :3], Tcw[:, 3]
+    Pi, Qi = R @ P + t, R @ Q + t
+    proj = lambda X: np.array([cx + fx * X[0] / X[2], cy + fy * X[1] / X[2]])
+    p, q = proj(Pi), proj(Qi)
+    e = np.array([lo[0] * p[0] + lo[1] * p[1] + lo[2], lo[0] * q[0] + lo[1] * q[1] + lo[2]])
+    r = np.linalg.norm(e)
+    fxlx, fyly = fx * e[0], fy * e[1]
+    m = max(hth, r)
+
+    def rows(G, ek):
+        gx, gy, gz = G
+        gz2 = 1.0 / max(hth, gz * gz)
+        Jpose = np.array([gz2 * fxlx * gz, gz2 * fyly * gz, -gz2 * (fxlx * gx + fyly * gy),
+                          -gz2 * (fxlx * gx * gy + fyly * gy * gy + fyly * gz * gz),
+                          gz2 * (fxlx * gx * gx + fxlx * gz * gz + fyly * gx * gy),
+                          gz2 * (fyly * gx * gz - fxlx * gy * gz)])
+        J0 = np.array([gz2 * fxlx * gz, gz2 * fyly * gz, -gz2 * (fxlx * gx + fyly * gy)])
+        return Jpose, (J0 @ R) * ek / m
+    JPi, JPw = rows(Pi, e[0])
+    JQi, JQw = rows(Qi, e[1])
+    return r, 1 / (1 + r * r), (JPi * e[0] + JQi * e[1]) / m, np.concatenate([JPw, JQw])
+
+
+def test_gba_line_rows_match_literal_transcription():
+    from plba.hlm import gba_window
+    win = gba_window(synth.generate("C1L"))
+    g = win.graph
+    Tcw = g.kf_Tcw.reshape(-1, 3, 4)
+    for e in range(0, g.n_eln, 5):
+        kf, lm = g.eln_kf[e], g.eln_lm[e]
+        P, Q = win.ln_line3d[lm, :3], win.ln_line3d[lm, 3:]
+        got = oa.gba_line_obs(Tcw[kf], P, Q, g.eln_obs[e, :3], CAM)
+        ref = _gba_line_literal(Tcw[kf], P, Q, g.eln_obs[e, :3], CAM)
+        assert got[0] == pytest.approx(ref[0], rel=1e-12)
+        np.testing.assert_allclose(got[2], ref[2], rtol=1e-9, atol=1e-12 * np.abs(ref[2]).max())
+        np.testing.assert_allclose(got[3], ref[3], rtol=1e-9, atol=1e-12 * np.abs(ref[3]).max())
+
+
+@pytest.mark.parametrize("params", [{}, {"lambda0": 1e-7, "err_per_obs": 1}])
+def test_gba_block_solve_matches_dense_reference_matrix(params):
+    from plba.hlm import gba_window
+    win = gba_window(synth.generate("C1L"))
+    p = capi.gba_params(**params)
+    a = oa.hlm_lba(win, p)
+    b = oa.hlm_lba(win, p, dense=True)
+    for k, x0 in (("kf_x", win.kf_x), ("pt_xyz", win.graph.pt_xyz), ("ln_line3d", win.ln_line3d)):
+        assert _rel(a[k] - x0, b[k] - x0) < 1e-7, k
+    np.testing.assert_array_equal(a["trace"]["result"], b["trace"]["result"])
+
