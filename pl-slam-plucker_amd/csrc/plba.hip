@@ -41,11 +41,12 @@ namespace plba {
 
 enum KernelId {
     K_LINEARIZE, K_REDUCE, K_ITER_INIT, K_ESCHUR, K_MEMSET, K_ASSEMBLE, K_FINALIZE, K_FACTOR,
-    K_POSE_UPDATE, K_LM_UPDATE, K_EVAL, K_DECIDE, K_COUNT
+    K_POSE_UPDATE, K_LM_UPDATE, K_EVAL, K_DECIDE, K_DENSE_PANEL, K_DENSE_UPDATE, K_COUNT
 };
 static const char *kKernelNames[K_COUNT] = {
     "k_linearize", "k_iter_reduce", "k_iter_init", "k_edge_schur", "memset_rcs",
-    "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_lm_solve", "k_edge_eval", "k_decide"};
+    "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_lm_solve", "k_edge_eval", "k_decide",
+    "k_dense_panel", "k_dense_update"};
 
 }  // namespace plba
 
@@ -899,7 +900,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_lm, std::max(d.n_lms_blocks, 1));
     ALLOC(d.part_lms, d.n_lms_blocks);
     d.fold = sharded ? 0 : 1;
-    ZALLOC(d.cnt, 2 + (size_t)nblk);
+    d.fold_init = d.fold && !getenv("PLBA_NO_FOLD_INIT");
+    ZALLOC(d.cnt, 2 + (size_t)nblk + nf);  // arrival counters: lm_solve, iter_reduce, RCS blocks, poses
     d.n_ps = std::max(d.n_kf_blocks, d.bcr_N);
     ZALLOC(d.part_ps, d.n_ps);
     ZALLOC(d.ctrl, 1);
@@ -1002,7 +1004,9 @@ int launch_step(plba_ctx *ctx) {
         LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kInitNT), 0, s, d));
         COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 43 + 2 + d.nranks);
     }
-    LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kInitNT), 0, s, d));
+    const bool reduced = d.nf > 0 || d.n_lm > 0;
+    if (!(d.fold_init && reduced))  // (folded into the last k_iter_reduce workgroup otherwise)
+        LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kInitNT), 0, s, d));
     if (d.n_lm > 0) {
         LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     }
@@ -1015,18 +1019,19 @@ int launch_step(plba_ctx *ctx) {
         }
         if (!(d.fold && d.nch > 0))  // (folded into the last chunk of each block otherwise)
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
+        const size_t solve_lds = d.n <= kSolveLdsN ? sizeof(double) * (size_t)d.n : 0;  // y of dense_solve_wg
         if (d.band_mode) {
             LAUNCH(K_FACTOR, launch_band(d, s));
         } else if (d.dense_mfma) {  // blocked LDLᵀ, MFMA trailing updates (plba_dense.hpp)
             for (int K = 0; K < d.ntiles; ++K) {
-                LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_dense_panel, dim3(d.ntiles - K), dim3(kDensePanelNT), 0, s, d, K));
+                LAUNCH(K_DENSE_PANEL, hipLaunchKernelGGL(k_dense_panel, dim3((d.ntiles - K + 1) / 2), dim3(kDensePanelNT), 0, s, d, K));
                 const int m = d.ntiles - K - 1;
                 if (m > 0)
-                    LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, d, K));
+                    LAUNCH(K_DENSE_UPDATE, hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, d, K));
             }
-            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_dense_solve, dim3(1), dim3(kFacThreads), 0, s, d));
+            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_dense_solve, dim3(1), dim3(kFacThreads), solve_lds, s, d));
         } else {
-            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), 0, s, d));
+            LAUNCH(K_FACTOR, hipLaunchKernelGGL(k_rcs_factor, dim3(1), dim3(kFacThreads), solve_lds, s, d));
         }
     }
     // the factorisation kernels end with the pose update; without free poses it runs alone

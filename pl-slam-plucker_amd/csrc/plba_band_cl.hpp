@@ -35,10 +35,6 @@ __host__ __device__ constexpr size_t cl_lds_doubles(int bw) {
            2 * ((size_t)(bw + 1) * 36 + 6);
 }
 
-__device__ __forceinline__ double readlane_f64(double x, int l) {
-    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
-                            __builtin_amdgcn_readlane(__double2loint(x), l));
-}
 // v_rcp_f64 + one Newton step (the estimate is good to ~2^-26, one step squares the error)
 __device__ __forceinline__ double rcp_nr1(double x) {
     const double r = __builtin_amdgcn_rcp(x);

@@ -4,8 +4,8 @@
 // a loop apart share landmarks) factorise the RCS S (n = 6·nf, column-major
 // `Ad`, lower triangle) as a right-looking blocked LDLᵀ with 32×32 tiles, two launches per
 // panel K (captured in the step graph like every other kernel):
-//   k_dense_panel<K>   one workgroup per row tile I >= K: LDLᵀ of the diagonal tile S_KK in LDS
-//                      (every workgroup redundantly — 32 steps, cheaper than a third launch),
+//   k_dense_panel<K>   one wave per two row tiles I >= K: LDLᵀ of the diagonal tile S_KK in
+//                      registers (every workgroup redundantly — cheaper than a third launch),
 //                      then W_IK = S_IK·L_KK⁻ᵀ (= L_IK·D_K) and L_IK = W_IK·D_K⁻¹ (I > K);
 //   k_dense_update<K>  one wave per trailing tile (I, J), K < J <= I: S_IJ -= W_IK·L_JKᵀ with
 //                      v_mfma_f64_16x16x4_f64 (2×2 blocks of 16×16, eight k-steps of 4), W and
@@ -21,80 +21,80 @@
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 constexpr int kDT = 32;          // tile
-constexpr int kDensePanelNT = 256;
+constexpr int kDensePanelNT = 64;  // one wave: two row tiles per workgroup
 
-// LDLᵀ of the kb×kb lower tile T (in LDS, padded rows) in place: strict lower T[r][c] = L·D
-// (not yet divided), diagonal = D. Returns false on a zero pivot.
-template <int NT>
-__device__ __forceinline__ bool dense_tile_ldlt(double (*T)[kDT + 1], int kb, int *s_fail) {
-    const int tid = threadIdx.x;
-    for (int j = 0; j < kb; ++j) {
-        __syncthreads();
-        const double djj = T[j][j];
-        if (djj == 0.0) {
-            if (tid == 0) *s_fail = 1;
-        } else {
-            for (int e = tid; e < kDT * kDT; e += NT) {
-                const int r = e / kDT, c = e % kDT;
-                if (r > j && c > j && c <= r && r < kb) T[r][c] -= (T[r][j] / djj) * T[c][j];
-            }
-        }
-    }
-    __syncthreads();
-    return *s_fail == 0;
-}
-
+// One wave per pair of row tiles (I0 = K + 2·blockIdx.x, I1 = I0 + 1), everything in registers:
+// lane l holds row l&31 of the diagonal tile S_KK and factorises it (every workgroup
+// redundantly, right-looking, the pivot column broadcast with v_readlane), then row l&31 of the
+// off-diagonal tile S_IK (I = I0 + (l>>5)) is solved against it, W = S_IK·L_KK⁻ᵀ by forward
+// substitution along the row (L_KK entries broadcast the same way). Fully unrolled: register
+// arrays need compile-time indices; no LDS, no barriers.
 __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
     TRIAL_GUARD
     if (K > 0 && d.ctrl->solve_ok == 0) return;  // an earlier panel hit a zero pivot
-    __shared__ double T[kDT][kDT + 1];
-    __shared__ double A[kDT][kDT + 1];
-    __shared__ double Dk[kDT];
-    __shared__ int s_fail;
-    const int tid = threadIdx.x, n = d.n;
-    const int I = K + blockIdx.x;
+    const int lane = threadIdx.x, r = lane & 31, n = d.n;
     const int k0 = K * kDT, kb = min(kDT, n - k0);
-    const int i0 = I * kDT, ib = min(kDT, n - i0);
+    const int I = K + 2 * (int)blockIdx.x + (lane >> 5);
+    const int i0 = I * kDT;
     double *Ad = d.Ad;
-    if (tid == 0) s_fail = 0;
-    for (int e = tid; e < kDT * kDT; e += kDensePanelNT) {  // column-major source: c outer, r inner
-        const int c = e / kDT, r = e % kDT;
-        T[r][c] = (r < kb && c <= r) ? Ad[(size_t)(k0 + r) + (size_t)(k0 + c) * n] : 0.0;
-        if (I > K) A[r][c] = (r < ib && c < kb) ? Ad[(size_t)(i0 + r) + (size_t)(k0 + c) * n] : 0.0;
+    // loads at clamped (always valid) addresses, selected after: no per-element branches
+    double t[kDT];
+    {
+        const double *row = Ad + (size_t)(k0 + min(r, kb - 1)) + (size_t)k0 * n;
+#pragma unroll
+        for (int c = 0; c < kDT; ++c) t[c] = row[(size_t)min(c, kb - 1) * n];
     }
-    const bool ok = dense_tile_ldlt<kDensePanelNT>(T, kb, &s_fail);
+#pragma unroll
+    for (int c = 0; c < kDT; ++c)  // row r, lower part; rows past kb are identity rows
+        t[c] = (r < kb && c <= r) ? t[c] : (c == r ? 1.0 : 0.0);
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < kDT; ++j) {
+        const double djj = readlane_f64(t[j], j);  // wave-uniform
+        ok = ok && djj != 0.0;
+        const double lrj = r > j ? t[j] * (1.0 / djj) : 0.0;
+#pragma unroll
+        for (int c = j + 1; c < kDT; ++c) {
+            const double tcj = readlane_f64(t[j], c);
+            if (r >= c) t[c] -= lrj * tcj;
+        }
+    }
+    // t[p] (p < r) = L[r][p]·D_p -> L[r][p]; t[r] = D_r
+    double D[kDT];
+#pragma unroll
+    for (int p = 0; p < kDT; ++p) D[p] = readlane_f64(t[p], p);
+#pragma unroll
+    for (int p = 0; p < kDT; ++p)
+        if (p < r) t[p] = t[p] / D[p];
     if (blockIdx.x == 0) {
-        if (tid == 0 && (K == 0 || !ok)) d.ctrl->solve_ok = ok ? 1 : 0;
-        if (!ok) return;
-        for (int e = tid; e < kDT * kDT; e += kDensePanelNT) {  // L (strict lower) and D
-            const int c = e / kDT, r = e % kDT;
-            if (r < kb && c <= r)
-                Ad[(size_t)(k0 + r) + (size_t)(k0 + c) * n] = r == c ? T[r][r] : T[r][c] / T[c][c];
-        }
-        return;
-    }
-    if (!ok) return;
-    if (tid < kDT) Dk[tid] = tid < kb ? T[tid][tid] : 1.0;
-    __syncthreads();
-    // W = A·L⁻ᵀ row by row (L unit lower: L[c][p] = T[c][p]/D_p), 8 threads per row: thread q of
-    // row r owns columns c ≡ q (mod 8); column c needs W[r][p<c] — kept in LDS (A is overwritten)
-    const int r = tid / 8, q = tid % 8;
-    for (int c = 0; c < kb; ++c) {
-        if (r < ib && (c & 7) == q) {
-            double w = A[r][c];
-            for (int p = 0; p < c; ++p) w -= A[r][p] * (T[c][p] / Dk[p]);
-            A[r][c] = w;
-        }
-        __syncthreads();
-    }
-    for (int e = tid; e < kDT * kDT; e += kDensePanelNT) {
-        const int c = e / kDT, rr = e % kDT;
-        if (rr < ib && c < kb) {
-            const double w = A[rr][c];
-            Ad[(size_t)(i0 + rr) + (size_t)(k0 + c) * n] = w / Dk[c];  // L_IK
-            d.Wbuf[(size_t)(i0 + rr) * kTile + c] = w;                // W_IK = L_IK·D_K
+        if (lane == 0 && (K == 0 || !ok)) d.ctrl->solve_ok = ok ? 1 : 0;
+        if (ok && lane < 32 && r < kb) {
+#pragma unroll
+            for (int c = 0; c < kDT; ++c)
+                if (c <= r) Ad[(size_t)(k0 + r) + (size_t)(k0 + c) * n] = t[c];
         }
     }
+    if (!ok || I == K || I >= d.ntiles) return;
+    const bool live = i0 + r < n;
+    double a[kDT];
+    {
+        const double *row = Ad + (size_t)min(i0 + r, n - 1) + (size_t)k0 * n;
+#pragma unroll
+        for (int c = 0; c < kDT; ++c) a[c] = row[(size_t)min(c, kb - 1) * n];
+    }
+#pragma unroll
+    for (int c = 0; c < kDT; ++c) a[c] = (live && c < kb) ? a[c] : 0.0;
+#pragma unroll
+    for (int c = 1; c < kDT; ++c)
+#pragma unroll
+        for (int p = 0; p < c; ++p) a[c] -= a[p] * readlane_f64(t[p], c);  // L[c][p]
+    if (!live) return;
+#pragma unroll
+    for (int c = 0; c < kDT; ++c)
+        if (c < kb) {
+            d.Wbuf[(size_t)(i0 + r) * kTile + c] = a[c];                     // W_IK = L_IK·D_K (row-major)
+            Ad[(size_t)(i0 + r) + (size_t)(k0 + c) * n] = a[c] / D[c];       // L_IK
+        }
 }
 
 // trailing tile index t -> (I, J) with K < J <= I < nt, row-major over the lower triangle
@@ -157,7 +157,10 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
 // forward / backward substitution through the dense factor + pose update (one workgroup)
 __global__ __launch_bounds__(kFacThreads) void k_dense_solve(Dev d) {
     TRIAL_GUARD
-    if (d.ctrl->solve_ok) dense_solve_wg(d);
+    if (d.ctrl->solve_ok) {
+        if (d.n <= kSolveLdsN) dense_solve_wg<true>(d);
+        else dense_solve_wg<false>(d);
+    }
     __syncthreads();
     pose_update_wg<kFacThreads>(d);  // applied even after a failed solve, with the previous x_p (A13)
 }

@@ -136,7 +136,8 @@ struct Dev {
     int32_t n_ps;                       // max(n_kf_blocks, bcr_N)
     int32_t fold;                       // 1: k_rcs_finalize / k_decide run as the tails of the
                                         //    preceding launch (last arriver); 0 when sharded
-    int32_t *cnt;                       // [2 + nblk] arrival counters: lm_solve, (spare), per RCS block
+    int32_t fold_init;                  // 1: k_iter_init runs as the tail of k_iter_reduce
+    int32_t *cnt;                       // [2 + nblk + nf] arrival counters: lm_solve, iter_reduce, per RCS block, per pose
     int32_t *h_kf;                      // [nf] keyframe of each free-pose Hessian index
     Ctrl *ctrl;
     plba_iter_trace *trace;             // [kTraceCap] per-iteration records written by k_decide
@@ -463,7 +464,38 @@ __device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
     if (threadIdx.x == 0) {
         double *o = d.pose_part + ((size_t)h * kPoseParts + part) * kPP;
 #pragma unroll
-        for (int k = 0; k < kPP; ++k) o[k] = acc[k];
+        for (int k = 0; k < kPP; ++k) st_sc1(o + k, acc[k]);  // read by the pose's combine below
+    }
+    // folded iteration init: the last of the pose's kPoseParts workgroups adds the parts (in part
+    // order, as pose_combine does) into Hpp / b_p / active count and publishes max|Hpp_jj|
+    if (d.fold_init && arrive_last(d.cnt + 2 + d.nblk + h, kPoseParts)) {
+        const int k = threadIdx.x;
+        double v = 0.0;
+        if (k < kPP) {
+            const double *src = d.pose_part + (size_t)h * kPoseParts * kPP + k;
+            double p[kPoseParts];
+#pragma unroll
+            for (int j = 0; j < kPoseParts; ++j) p[j] = ld_sc1(src + j * kPP);
+            v = p[0];
+#pragma unroll
+            for (int j = 1; j < kPoseParts; ++j) v += p[j];
+            if (k < 21) {
+                int r = 0, rem = k;
+                while (rem >= 6 - r) { rem -= 6 - r; ++r; }
+                const int cc = r + rem;
+                d.Hpp_w[(size_t)h * 36 + r * 6 + cc] = v;
+                d.Hpp_w[(size_t)h * 36 + cc * 6 + r] = v;
+                if (r != cc) v = 0.0;
+            } else if (k < 27) {
+                d.bp_w[(size_t)h * 6 + (k - 21)] = v;
+                v = 0.0;
+            } else {
+                d.pact_w[h] = v;
+                v = 0.0;
+            }
+        }
+        const double m = wave_max(fabs(v));  // kLmBlock = one wave
+        if (threadIdx.x == 0) st_sc1(d.part_max + h, m);
     }
 }
 
@@ -544,28 +576,22 @@ __device__ __forceinline__ void landmark_reduce(const Dev &d, int lb) {
     double m = block_max<kLmBlock>(mx, sh);
     const int anyb = __syncthreads_or(any ? 1 : 0);
     if (threadIdx.x == 0) {
-        d.part_max[d.nf + lb] = m;
-        d.part_any[lb] = anyb;
+        st_sc1(d.part_max + d.nf + lb, m);
+        __hip_atomic_store(d.part_any + lb, anyb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-__global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
-    ITER_GUARD
-    const int b = blockIdx.x, np = kPoseParts * d.nf;
-    if (b < np) pose_partial(d, b / kPoseParts, b % kPoseParts);  // workgroup-uniform branch
-    else landmark_reduce(d, b - np);
-}
 
 // Hpp, b_p from the pose parts (added in part order); returns this thread's max |Hpp_jj|
-template <int NT>
+template <int NT, bool SC1 = false>
 __device__ __forceinline__ double pose_combine(const Dev &d, double *H, double *bp) {
     double m = 0.0;
     for (int i = threadIdx.x; i < d.nf * kPP; i += NT) {
         const int h = i / kPP, k = i % kPP;
         const double *src = d.pose_part + (size_t)h * kPoseParts * kPP + k;
-        double v = src[0];
+        double v = SC1 ? ld_sc1(src) : src[0];
 #pragma unroll
-        for (int j = 1; j < kPoseParts; ++j) v += src[j * kPP];
+        for (int j = 1; j < kPoseParts; ++j) v += SC1 ? ld_sc1(src + j * kPP) : src[j * kPP];
         if (k < 21) {
             int r = 0, rem = k;
             while (rem >= 6 - r) { rem -= 6 - r; ++r; }
@@ -606,28 +632,64 @@ __global__ __launch_bounds__(kInitNT) void k_iter_pack(Dev d) {
     for (int r = threadIdx.x; r < d.nranks; r += kInitNT) o[2 + r] = r == d.rank ? mx : 0.0;
 }
 
-__global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
-    ITER_GUARD
-    __shared__ double sh[kInitNT / 64];
+// the iteration init (k_iter_init's work): run as its own launch (sharded windows, windows with
+// nothing to reduce) or as the tail of the last-arriving k_iter_reduce workgroup (SC1: the
+// partials of that launch are read write-through)
+template <int NT, bool SC1>
+__device__ __forceinline__ void iter_init_body(const Dev &d, double *sh) {
     double chi, mx;
     bool any;
     if (d.sharded) {  // totals from the all-reduced iteration array
         const double *o = d.red_iter + (size_t)d.nf * 43;
         double m = 0.0;
-        for (int i = threadIdx.x; i < d.nf * 6; i += kInitNT) m = fmax(m, fabs(d.Hpp[(i / 6) * 36 + (i % 6) * 7]));
-        for (int r = threadIdx.x; r < d.nranks; r += kInitNT) m = fmax(m, o[2 + r]);
-        mx = block_max<kInitNT>(m, sh);
+        for (int i = threadIdx.x; i < d.nf * 6; i += NT) m = fmax(m, fabs(d.Hpp[(i / 6) * 36 + (i % 6) * 7]));
+        for (int r = threadIdx.x; r < d.nranks; r += NT) m = fmax(m, o[2 + r]);
+        mx = block_max<NT>(m, sh);
         chi = o[0];
         any = o[1] != 0.0;
-    } else {
-        double m = pose_combine<kInitNT>(d, d.Hpp_w, d.bp_w);
-        double s = 0.0;
-        for (int i = threadIdx.x; i < d.n_lin_blocks; i += kInitNT) s += d.part_chi2[i];
-        chi = block_sum<kInitNT>(s, sh);
-        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) m = fmax(m, d.part_max[d.nf + i]);
-        mx = block_max<kInitNT>(m, sh);
+    } else if (SC1) {
+        // folded: the pose maxima are in part_max[0, nf) (per-pose combine), the landmark ones
+        // after them; every partial of this launch is read write-through, U loads in flight
+        constexpr int U = 8;
+        double s = 0.0, m = 0.0;
         int a = 0;
-        for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) a |= d.part_any[i];
+        for (int i0 = threadIdx.x; i0 < d.n_lin_blocks; i0 += NT * U) {
+            double v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = i0 + u * NT < d.n_lin_blocks ? d.part_chi2[i0 + u * NT] : 0.0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) s += v[u];
+        }
+        const int nm = d.nf + d.n_lm_blocks;
+        for (int i0 = threadIdx.x; i0 < nm; i0 += NT * U) {
+            double v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = i0 + u * NT < nm ? ld_sc1(d.part_max + i0 + u * NT) : 0.0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) m = fmax(m, v[u]);
+        }
+        for (int i0 = threadIdx.x; i0 < d.n_lm_blocks; i0 += NT * U) {
+            int v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                v[u] = i0 + u * NT < d.n_lm_blocks
+                           ? __hip_atomic_load(d.part_any + i0 + u * NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) a |= v[u];
+        }
+        chi = block_sum<NT>(s, sh);
+        mx = block_max<NT>(m, sh);
+        any = __syncthreads_or(a) != 0;
+    } else {
+        double m = pose_combine<NT>(d, d.Hpp_w, d.bp_w);
+        double s = 0.0;
+        for (int i = threadIdx.x; i < d.n_lin_blocks; i += NT) s += d.part_chi2[i];
+        chi = block_sum<NT>(s, sh);
+        for (int i = threadIdx.x; i < d.n_lm_blocks; i += NT) m = fmax(m, d.part_max[d.nf + i]);
+        mx = block_max<NT>(m, sh);
+        int a = 0;
+        for (int i = threadIdx.x; i < d.n_lm_blocks; i += NT) a |= d.part_any[i];
         any = __syncthreads_or(a) != 0;
     }
     if (threadIdx.x == 0) {
@@ -684,6 +746,22 @@ __global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
         c->broke = 0;
         c->need_iter = 0;
     }
+}
+__global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
+    ITER_GUARD
+    __shared__ double sh[kInitNT / 64];
+    iter_init_body<kInitNT, false>(d, sh);
+}
+
+__global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
+    ITER_GUARD
+    __shared__ double sh_init[kLmBlock / 64];
+    const int b = blockIdx.x, np = kPoseParts * d.nf;
+    if (b < np) pose_partial(d, b / kPoseParts, b % kPoseParts);  // workgroup-uniform branch
+    else landmark_reduce(d, b - np);
+    // the last workgroup to finish runs the iteration init (k_iter_init's work; the pose
+    // combine already ran per pose)
+    if (d.fold_init && arrive_last(d.cnt + 1, (int32_t)gridDim.x)) iter_init_body<kLmBlock, true>(d, sh_init);
 }
 
 // ---------------------------------------------------------------- reduced camera system
@@ -882,35 +960,63 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
 }
 
 constexpr int kFacThreads = 1024;
+constexpr int kSolveLdsN = 6144;  // y held in (dynamic) LDS up to this n (48 KiB), in Wbuf beyond
 // ---- solve L D Lᵀ x = b_s through the envelope-aware dense factor in Ad (unit L below the
 // diagonal, D on it), tile by tile; one workgroup of kFacThreads. x -> xp.
-__device__ __noinline__ void dense_solve_wg(const Dev &d) {
+// Forward: wave 0 solves the diagonal tile (its row of L in registers, y_j broadcast by
+// readlane) while the other waves prefetch their rows' coefficients of the tile's columns
+// (independent of y); then those rows are updated. Backward: 32 partial column sums per tile
+// (lanes along rows), then wave 0 adds them and solves the tile. y lives in LDS (LY).
+template <bool LY>
+__device__ __forceinline__ void dense_solve_wg(const Dev &d) {
+    extern __shared__ double y_lds[];
     __shared__ double red[kFacThreads / kTile][kTile + 1];
     const int tid = threadIdx.x;
     const int n = d.n;
     const int nt = d.ntiles;
     const double *Ad = d.Ad;
-    double *y = d.Wbuf;  // reuse: y[0..n)
+    double *y = LY ? y_lds : d.Wbuf;
     for (int i = tid; i < n; i += kFacThreads) y[i] = d.bs[i];
     __syncthreads();
-    // forward: tile by tile
+    constexpr int kRowThreads = kFacThreads - 64;
     for (int K = 0; K < nt; ++K) {
         const int k0 = K * kTile, kb = min(kTile, n - k0);
-        if (tid < 64) {  // one wave solves the diagonal tile
+        const int fend = min(n, (d.tile_last[K] + 1) * kTile);
+        const int i1 = k0 + kb + tid - 64;  // this thread's first row of the update
+        double cf[kTile];
+        if (tid < 64) {
             double yi = (tid < kb) ? y[k0 + tid] : 0.0;
-            for (int j = 0; j < kb; ++j) {
-                const double yj = __shfl(yi, j, 64);
-                if (tid > j && tid < kb) yi -= Ad[(size_t)(k0 + tid) + (size_t)(k0 + j) * n] * yj;
+            // loads at clamped (always valid) addresses, selected after: no per-element branches
+            const double *row = Ad + (size_t)(k0 + min(tid, kb - 1)) + (size_t)k0 * n;
+            double l[kTile];
+#pragma unroll
+            for (int j = 0; j < kTile; ++j) l[j] = row[(size_t)min(j, kb - 1) * n];
+#pragma unroll
+            for (int j = 0; j < kTile; ++j) {
+                const double yj = readlane_f64(yi, j);
+                if (tid > j && tid < kb) yi -= l[j] * yj;
             }
             if (tid < kb) y[k0 + tid] = yi;
+        } else {
+            const double *row = Ad + (size_t)min(i1, n - 1) + (size_t)k0 * n;
+#pragma unroll
+            for (int p = 0; p < kTile; ++p) cf[p] = row[(size_t)min(p, kb - 1) * n];
         }
         __syncthreads();
-        const int fend = min(n, (d.tile_last[K] + 1) * kTile);
-        for (int i = k0 + kb + tid; i < fend; i += kFacThreads) {
-            if (d.tile_first[i / kTile] > K) continue;
-            double s = 0.0;
-            for (int p = 0; p < kb; ++p) s += Ad[(size_t)i + (size_t)(k0 + p) * n] * y[k0 + p];
-            y[i] -= s;
+        if (tid >= 64) {
+            if (i1 < fend && d.tile_first[i1 / kTile] <= K) {
+                double s = 0.0;
+#pragma unroll
+                for (int p = 0; p < kTile; ++p)
+                    if (p < kb) s += cf[p] * y[k0 + p];
+                y[i1] -= s;
+            }
+            for (int i = i1 + kRowThreads; i < fend; i += kRowThreads) {  // n > ~kFacThreads only
+                if (d.tile_first[i / kTile] > K) continue;
+                double s = 0.0;
+                for (int p = 0; p < kb; ++p) s += Ad[(size_t)i + (size_t)(k0 + p) * n] * y[k0 + p];
+                y[i] -= s;
+            }
         }
         __syncthreads();
     }
@@ -920,30 +1026,39 @@ __device__ __noinline__ void dense_solve_wg(const Dev &d) {
     for (int K = nt - 1; K >= 0; --K) {
         const int k0 = K * kTile, kb = min(kTile, n - k0);
         // y_K -= Σ_{i > tile} L[i][k] y[i]   (column k of L below the tile): 32 partial sums per
-        // column (rows i ≡ part mod 32), added in part order
+        // column (rows i ≡ part mod 32), added in part order; part runs along the lanes so a
+        // wave reads two columns, 32 consecutive rows each
         const int bend = min(n, (d.tile_last[K] + 1) * kTile);
         {
-            const int c = tid % kTile, part = tid / kTile;
+            const int part = tid % kTile, c = tid / kTile;
             double s = 0.0;
-            if (c < kb)
+            if (c < kb) {
+#pragma unroll 4
                 for (int i = k0 + kb + part; i < bend; i += kFacThreads / kTile) {
                     if (d.tile_first[i / kTile] > K) continue;
                     s += Ad[(size_t)i + (size_t)(k0 + c) * n] * y[i];
                 }
+            }
             red[part][c] = s;
         }
-        __syncthreads();
-        if (tid < kb) {
-            double s = 0.0;
-            for (int p = 0; p < kFacThreads / kTile; ++p) s += red[p][tid];
-            y[k0 + tid] -= s;
+        double l[kTile];
+        if (tid < 64) {  // column of L of the diagonal tile in registers
+            const double *col = Ad + (size_t)k0 + (size_t)(k0 + min(tid, kb - 1)) * n;
+#pragma unroll
+            for (int j = 0; j < kTile; ++j) l[j] = col[min(j, kb - 1)];
         }
         __syncthreads();
         if (tid < 64) {
-            double yi = (tid < kb) ? y[k0 + tid] : 0.0;
-            for (int j = kb - 1; j >= 0; --j) {
-                const double yj = __shfl(yi, j, 64);
-                if (tid < j) yi -= Ad[(size_t)(k0 + j) + (size_t)(k0 + tid) * n] * yj;
+            double yi = 0.0;
+            if (tid < kb) {
+                double s = 0.0;
+                for (int p = 0; p < kFacThreads / kTile; ++p) s += red[p][tid];
+                yi = y[k0 + tid] - s;
+            }
+#pragma unroll
+            for (int j = kTile - 1; j >= 0; --j) {
+                const double yj = readlane_f64(yi, j);
+                if (tid < j && j < kb) yi -= l[j] * yj;
             }
             if (tid < kb) y[k0 + tid] = yi;
         }
@@ -1040,7 +1155,10 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
     }
     __syncthreads();
     if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
-    if (!s_fail) dense_solve_wg(d);  // on failure x_p keeps its previous value (g2o leaves _x untouched)
+    if (!s_fail) {  // on failure x_p keeps its previous value (g2o leaves _x untouched)
+        if (n <= kSolveLdsN) dense_solve_wg<true>(d);
+        else dense_solve_wg<false>(d);
+    }
     __syncthreads();
     pose_update_wg<kFacThreads>(d);  // the update is applied even after a failed solve (A13)
 }

@@ -21,6 +21,12 @@
 
 namespace plba {
 
+// broadcast lane l's value (l must be wave-uniform)
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                            __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+
 struct Cam {
     double fx, fy, cx, cy;
 };
