@@ -18,8 +18,6 @@
 // B lane l -> B[k=l>>4][l&15]; C/D (f64 form) reg i -> row (l>>4)+4i, col l&15.
 #pragma once
 
-typedef double dbl4 __attribute__((ext_vector_type(4)));
-
 constexpr int kDT = 32;          // tile
 constexpr int kDensePanelNT = 64;  // one wave: two row tiles per workgroup
 

@@ -21,6 +21,8 @@
 
 namespace plba {
 
+typedef double dbl4 __attribute__((ext_vector_type(4)));  // v_mfma_f64_16x16x4 accumulator
+
 // broadcast lane l's value (l must be wave-uniform)
 __device__ __forceinline__ double readlane_f64(double x, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
