@@ -213,6 +213,58 @@ void plba_hlm_default_params(plba_hlm_params *p);
  * lambda_start / lambda_end around the iteration. */
 int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params *p, plba_hlm_result *res);
 
+/* ---- Loop-closure pose graph:
+ *   bool MapHandler::loopClosureOptimizationEssGraphG2O()  (src/mapHandler.cpp:5070-5299)
+ *   bool MapHandler::loopClosureOptimizationCovGraphG2O()  (src/mapHandler.cpp:5301-5531)
+ * g2o::SparseOptimizer with g2o::VertexSE3 vertices and g2o::EdgeSE3 edges,
+ * OptimizationAlgorithmLevenberg over BlockSolver_6_3 + LinearSolverCholmod,
+ * setUserLambdaInit(1e-10) (:5085), then initializeOptimization(); computeInitialGuess();
+ * computeActiveErrors(); optimize(maxItersPGO) (:5182-5185).
+ *   VertexSE3::oplusImpl:  X <- X · fromVectorMQT(δ),  δ = [Δt; qx qy qz]
+ *   EdgeSE3::computeError: e = toVectorMQT(Z⁻¹ · X_from⁻¹ · X_to), χ² = eᵀΩe
+ * Poses are Isometry3 (row-major 3x4 [R | t]). The reference replaces Cholmod's supernodal
+ * Cholesky here by a dense LDLᵀ on the device: same solution; the solve fails when a pivot is
+ * not positive (CHOLMOD_NOT_POSDEF), which g2o treats as a rejected trial. */
+typedef struct plba_pgo_graph {
+    int32_t        n_v;     /* vertices                                                         */
+    int32_t        n_e;     /* edges                                                            */
+    const int32_t *v_id;    /* [n_v] g2o vertex ids (the reference: KF indices), unique         */
+    const double  *v_T;     /* [n_v][12] VertexSE3 estimates                                    */
+    const uint8_t *v_fixed; /* [n_v] setFixed                                                   */
+    const int32_t *e_v;     /* [n_e][2] vertex positions (0..n_v-1) of vertex(0), vertex(1)     */
+    const double  *e_Z;     /* [n_e][12] setMeasurement                                         */
+    const double  *e_info;  /* [n_e][36] information, row-major; NULL = identity (the reference) */
+} plba_pgo_graph;
+
+typedef struct plba_pgo_params {
+    double  user_lambda_init; /* setUserLambdaInit: 1e-10 (:5085); <= 0: τ·max|H_ii|, τ = 1e-5   */
+    int32_t max_iters;        /* optimize(SlamConfig::maxItersPGO()) — 100 (src/slamConfig.cpp:79) */
+    int32_t initial_guess;    /* 1: computeInitialGuess() (the reference calls it)              */
+    int32_t max_trials;       /* OptimizationAlgorithmLevenberg maxTrialsAfterFailure: 10        */
+    int32_t pad;
+} plba_pgo_params;
+
+typedef struct plba_pgo_result {
+    double          *v_T;        /* [n_v][12] final estimates (NULL = not wanted)                */
+    plba_iter_trace *trace;      /* [trace_cap] per-iteration records (stage 0), may be NULL     */
+    int32_t          trace_cap;
+    int32_t          n_trace;
+    int32_t          iterations; /* outer iterations run by optimize()                          */
+    int32_t          trials;     /* damped trials run                                           */
+    int32_t          solve_fails;/* trials whose factorisation met a non-positive pivot         */
+    int32_t          n_free;     /* vertices in the Hessian (active, not fixed)                 */
+    double           chi2_initial; /* activeChi2 after computeInitialGuess                      */
+    double           chi2_final;
+    double           lambda_final;
+    double           solve_ms;   /* wall time of optimize()                                     */
+} plba_pgo_result;
+
+void plba_pgo_default_params(plba_pgo_params *p);
+/* computeInitialGuess (host: g2o's EstimatePropagator, Dijkstra from the fixed vertices over the
+ * active edges, unit edge cost) and optimize() on the device (per-edge linearisation, dense
+ * assembly, multi-workgroup LDLᵀ with MFMA trailing updates, one host decision per trial). */
+int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_params *p, plba_pgo_result *res);
+
 /* ---- Sharded windows: one context per GPU, one window split over nranks.
  * Landmarks (with all their edges) are partitioned by the keyframe range of their first
  * observation (kf_obs_list[0], the base KF of map_points_kf_idx); poses are replicated.

@@ -16,6 +16,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <numeric>
 #include <string>
@@ -112,6 +113,11 @@ struct plba_ctx {
     size_t ev_next = 0;
     double k_ms[K_COUNT] = {0};
     int32_t k_n[K_COUNT] = {0};
+    // loop-closure pose graph (plba_pgo_optimize): its own grow-only device block, independent
+    // of the window arena (a PGO call leaves an uploaded window intact)
+    char *pgo_mem = nullptr;
+    size_t pgo_cap = 0;
+    double *pgo_hout = nullptr;  // pinned [4]
 
     void set_error(const char *fmt, ...) {
         char buf[512];
@@ -1264,6 +1270,8 @@ int plba_destroy(plba_ctx *ctx) {
     if (ctx->staging) (void)hipHostFree(ctx->staging);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
+    if (ctx->pgo_mem) (void)hipFree(ctx->pgo_mem);
+    if (ctx->pgo_hout) (void)hipHostFree(ctx->pgo_hout);
     if (ctx->comm.hbuf) (void)hipHostFree(ctx->comm.hbuf);
     if (ctx->comm.nccl) (void)ncclCommDestroy(ctx->comm.nccl);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1699,6 +1707,370 @@ int plba_comm_init_host(plba_ctx *ctx, int32_t nranks, int32_t rank, plba_host_a
 int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on) {
     if (!ctx) return PLBA_E_INVALID;
     ctx->timing = on != 0;
+    return PLBA_OK;
+}
+
+// ---------------------------------------------------------------- loop-closure pose graph
+// MapHandler::loopClosureOptimization{EssGraph,CovGraph}G2O (src/mapHandler.cpp:5070-5531):
+// g2o SparseOptimizer::initializeOptimization / computeInitialGuess / optimize over VertexSE3 +
+// EdgeSE3 with OptimizationAlgorithmLevenberg (setUserLambdaInit) — device kernels in
+// csrc/plba_pgo.hpp, Levenberg decisions here.
+namespace {
+#pragma clang fp contract(off)
+struct HIso {
+    double R[9], t[3];
+};
+HIso hiso_load(const double *T) {
+    HIso a;
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) a.R[3 * r + c] = T[4 * r + c];
+        a.t[r] = T[4 * r + 3];
+    }
+    return a;
+}
+void hiso_store(const HIso &a, double *T) {
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) T[4 * r + c] = a.R[3 * r + c];
+        T[4 * r + 3] = a.t[r];
+    }
+}
+HIso hiso_mul(const HIso &a, const HIso &b) {
+    HIso o;
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) {
+            double s = 0.0;
+            for (int k = 0; k < 3; ++k) s = s + a.R[3 * r + k] * b.R[3 * k + c];
+            o.R[3 * r + c] = s;
+        }
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s = s + a.R[3 * r + k] * b.t[k];
+        o.t[r] = s + a.t[r];
+    }
+    return o;
+}
+HIso hiso_inv(const HIso &a) {
+    HIso o;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) o.R[3 * r + c] = a.R[3 * c + r];
+    for (int r = 0; r < 3; ++r) {
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s = s + o.R[3 * r + k] * a.t[k];
+        o.t[r] = -s;
+    }
+    return o;
+}
+}  // namespace
+
+void plba_pgo_default_params(plba_pgo_params *p) {
+    if (!p) return;
+    p->user_lambda_init = 1e-10;  // src/mapHandler.cpp:5085
+    p->max_iters = 100;           // SlamConfig::maxItersPGO(), src/slamConfig.cpp:79
+    p->initial_guess = 1;         // optimizer.computeInitialGuess(), :5183
+    p->max_trials = 10;           // g2o maxTrialsAfterFailure
+    p->pad = 0;
+}
+
+int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_params *pp, plba_pgo_result *res) {
+#pragma clang fp contract(off)
+    if (!ctx || !g || !res || g->n_v < 0 || g->n_e < 0) return PLBA_E_INVALID;
+    if ((g->n_v && (!g->v_id || !g->v_T || !g->v_fixed)) || (g->n_e && (!g->e_v || !g->e_Z))) return PLBA_E_INVALID;
+    plba_pgo_params prm;
+    if (pp) prm = *pp;
+    else plba_pgo_default_params(&prm);
+    if (prm.max_iters < 0 || prm.max_trials < 1) {
+        ctx->set_error("max_iters must be >= 0 and max_trials >= 1");
+        return PLBA_E_INVALID;
+    }
+    const int nv = g->n_v, ne = g->n_e;
+    for (int e = 0; e < 2 * ne; ++e)
+        if (g->e_v[e] < 0 || g->e_v[e] >= nv) {
+            ctx->set_error("pose-graph edge %d references vertex %d (n_v %d)", e / 2, g->e_v[e], nv);
+            return PLBA_E_INVALID;
+        }
+    {
+        std::vector<int32_t> ids(g->v_id, g->v_id + nv);
+        std::sort(ids.begin(), ids.end());
+        if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) {
+            ctx->set_error("duplicate pose-graph vertex id");
+            return PLBA_E_INVALID;
+        }
+    }
+    (void)hipSetDevice(ctx->opts.device);
+    const auto t0 = std::chrono::steady_clock::now();
+    // ---- SparseOptimizer::initializeOptimization(): active edges (not all vertices fixed) in
+    //      creation order; Hessian index of the active free vertices in id order
+    std::vector<HIso> X(nv), Z(ne), Zinv(ne);
+    for (int v = 0; v < nv; ++v) X[v] = hiso_load(g->v_T + 12 * (size_t)v);
+    for (int e = 0; e < ne; ++e) {
+        Z[e] = hiso_load(g->e_Z + 12 * (size_t)e);
+        Zinv[e] = hiso_inv(Z[e]);  // EdgeSE3::setMeasurement keeps the inverse
+    }
+    std::vector<int32_t> act;
+    std::vector<uint8_t> is_act(ne, 0);
+    std::vector<int> nact_v(nv, 0);
+    for (int e = 0; e < ne; ++e) {
+        const int a = g->e_v[2 * e], b = g->e_v[2 * e + 1];
+        if (g->v_fixed[a] && g->v_fixed[b]) continue;
+        act.push_back(e);
+        is_act[e] = 1;
+        ++nact_v[a];
+        ++nact_v[b];
+    }
+    std::vector<int> order(nv);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return g->v_id[a] < g->v_id[b]; });
+    std::vector<int32_t> hidx(nv, -1);
+    int nfree = 0;
+    for (int v : order)
+        if (nact_v[v] > 0 && !g->v_fixed[v]) hidx[v] = nfree++;
+    // ---- computeInitialGuess(): EstimatePropagator from the fixed vertices of the active edges
+    //      (std::set<Vertex*>: creation order), unit edge cost, multimap frontier (smallest
+    //      distance first, FIFO among equals), EdgeSE3::initialEstimate on each first reach
+    if (prm.initial_guess) {
+        std::vector<std::vector<int>> vedges(nv);
+        for (int e = 0; e < ne; ++e) {
+            vedges[g->e_v[2 * e]].push_back(e);
+            vedges[g->e_v[2 * e + 1]].push_back(e);
+        }
+        std::vector<int> roots;
+        std::vector<uint8_t> isroot(nv, 0);
+        for (int e : act)
+            for (int sd = 0; sd < 2; ++sd) {
+                const int v = g->e_v[2 * e + sd];
+                if (g->v_fixed[v] && !isroot[v]) { isroot[v] = 1; roots.push_back(v); }
+            }
+        std::sort(roots.begin(), roots.end());
+        const double inf = std::numeric_limits<double>::max();
+        std::vector<double> dist(nv, inf);
+        std::vector<int> level(nv, 0), pedge(nv, -1), parent(nv, -1);
+        std::multimap<double, int> frontier;
+        std::vector<std::multimap<double, int>::iterator> qit(nv);
+        std::vector<uint8_t> inq(nv, 0);
+        auto push = [&](int v) {
+            if (inq[v]) frontier.erase(qit[v]);
+            qit[v] = frontier.insert(frontier.upper_bound(dist[v]), {dist[v], v});
+            inq[v] = 1;
+        };
+        for (int r : roots) { dist[r] = 0.0; push(r); }
+        while (!frontier.empty()) {
+            const auto it = frontier.begin();
+            const int u = it->second;
+            frontier.erase(it);
+            inq[u] = 0;
+            if (level[u] > 0 && !g->v_fixed[u]) {
+                const int e = pedge[u];
+                if (parent[u] == g->e_v[2 * e]) X[u] = hiso_mul(X[g->e_v[2 * e]], Z[e]);
+                else X[u] = hiso_mul(X[g->e_v[2 * e + 1]], hiso_inv(Z[e]));
+            }
+            for (int e : vedges[u]) {
+                if (!is_act[e]) continue;
+                int maxf = -1;
+                for (int sd = 0; sd < 2; ++sd) {
+                    const int z = g->e_v[2 * e + sd];
+                    if (dist[z] != inf) maxf = std::max(maxf, level[z]);
+                }
+                for (int sd = 0; sd < 2; ++sd) {
+                    const int z = g->e_v[2 * e + sd];
+                    if (z == u) continue;
+                    const double zd = dist[u] + 1.0;
+                    if (zd < dist[z]) {
+                        dist[z] = zd;
+                        parent[z] = u;
+                        pedge[z] = e;
+                        level[z] = maxf + 1;
+                        push(z);
+                    }
+                }
+            }
+        }
+    }
+    // ---- blocks of H (lower triangle) and their contributions in edge order
+    std::map<std::pair<int, int>, std::vector<int32_t>> blocks;  // (col, row) -> contributions
+    for (int h = 0; h < nfree; ++h) blocks[{h, h}];
+    for (int e : act) {
+        const int hi = hidx[g->e_v[2 * e]], hj = hidx[g->e_v[2 * e + 1]];
+        if (hi >= 0) blocks[{hi, hi}].push_back(e << 2 | 0);
+        if (hj >= 0) blocks[{hj, hj}].push_back(e << 2 | 1);
+        if (hi >= 0 && hj >= 0 && hi != hj) {
+            if (hi > hj) blocks[{hj, hi}].push_back(e << 2 | 2);  // row block = vertex i
+            else blocks[{hi, hj}].push_back(e << 2 | 3);          // row block = vertex j
+        }
+    }
+    std::vector<int32_t> blk_r, blk_c, blk_off{0}, blk_con;
+    for (auto &kv : blocks) {
+        blk_c.push_back(kv.first.first);
+        blk_r.push_back(kv.first.second);
+        for (int32_t c : kv.second) blk_con.push_back(c);
+        blk_off.push_back((int32_t)blk_con.size());
+    }
+    const int n = 6 * nfree, nblk = (int)blk_r.size(), ntiles = (n + kTile - 1) / kTile;
+    const int nact = (int)act.size();
+    // ---- device block (grow-only)
+    struct Slot {
+        void **p;
+        size_t bytes;
+    };
+    PgoDev P{};
+    Dev dd{};
+    double *T0, *T1, *Ad;
+    int32_t *e_v_d, *act_d, *hidx_d, *blk_r_d, *blk_c_d, *blk_off_d, *blk_con_d, *tf_d, *tl_d;
+    double *Zinv_d, *info_d;
+    Ctrl *ctrl_d;
+    std::vector<Slot> slots = {
+        {(void **)&e_v_d, sizeof(int32_t) * 2 * (size_t)ne}, {(void **)&act_d, sizeof(int32_t) * (size_t)nact},
+        {(void **)&hidx_d, sizeof(int32_t) * (size_t)nv}, {(void **)&blk_r_d, sizeof(int32_t) * (size_t)nblk},
+        {(void **)&blk_c_d, sizeof(int32_t) * (size_t)nblk}, {(void **)&blk_off_d, sizeof(int32_t) * (size_t)(nblk + 1)},
+        {(void **)&blk_con_d, sizeof(int32_t) * blk_con.size()}, {(void **)&tf_d, sizeof(int32_t) * (size_t)ntiles},
+        {(void **)&tl_d, sizeof(int32_t) * (size_t)ntiles}, {(void **)&Zinv_d, sizeof(double) * 12 * (size_t)ne},
+        {(void **)&info_d, sizeof(double) * 36 * (size_t)ne}, {(void **)&T0, sizeof(double) * 12 * (size_t)nv},
+        {(void **)&T1, sizeof(double) * 12 * (size_t)nv}, {(void **)&P.eH, sizeof(double) * 144 * (size_t)ne},
+        {(void **)&P.eg, sizeof(double) * 12 * (size_t)ne}, {(void **)&P.echi, sizeof(double) * (size_t)ne},
+        {(void **)&P.Hd, sizeof(double) * (size_t)n * n}, {(void **)&Ad, sizeof(double) * (size_t)n * n},
+        {(void **)&P.b, sizeof(double) * (size_t)n}, {(void **)&P.x, sizeof(double) * (size_t)n},
+        {(void **)&dd.Wbuf, sizeof(double) * (size_t)std::max(n, 1) * kTile}, {(void **)&P.out, sizeof(double) * 4},
+        {(void **)&ctrl_d, sizeof(Ctrl)}};
+    size_t tot = 0;
+    for (auto &sl : slots) tot += (std::max(sl.bytes, (size_t)128) + 255) & ~(size_t)255;
+    if (tot > ctx->pgo_cap) {
+        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+        if (ctx->pgo_mem) (void)hipFree(ctx->pgo_mem);
+        ctx->pgo_mem = nullptr;
+        ctx->pgo_cap = 0;
+        if (hipMalloc((void **)&ctx->pgo_mem, tot) != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->set_error("pose graph: cannot allocate %zu bytes", tot);
+            return PLBA_E_NOMEM;
+        }
+        ctx->pgo_cap = tot;
+    }
+    if (!ctx->pgo_hout) PLBA_CHECK(hipHostMalloc((void **)&ctx->pgo_hout, sizeof(double) * 4));
+    {
+        size_t off = 0;
+        for (auto &sl : slots) {
+            *sl.p = ctx->pgo_mem + off;
+            off += (std::max(sl.bytes, (size_t)128) + 255) & ~(size_t)255;
+        }
+    }
+    hipStream_t s = ctx->stream;
+    std::vector<double> Tv(12 * (size_t)nv), Zi(12 * (size_t)ne), Om(36 * (size_t)ne);
+    for (int v = 0; v < nv; ++v) hiso_store(X[v], &Tv[12 * (size_t)v]);
+    for (int e = 0; e < ne; ++e) {
+        hiso_store(Zinv[e], &Zi[12 * (size_t)e]);
+        for (int k = 0; k < 36; ++k) Om[36 * (size_t)e + k] = g->e_info ? g->e_info[36 * (size_t)e + k] : (k % 7 == 0 ? 1.0 : 0.0);
+    }
+    std::vector<int32_t> tf(ntiles, 0), tl(ntiles, ntiles - 1);
+    auto up = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+    };
+    PLBA_CHECK(up(e_v_d, g->e_v, sizeof(int32_t) * 2 * (size_t)ne));
+    PLBA_CHECK(up(act_d, act.data(), sizeof(int32_t) * act.size()));
+    PLBA_CHECK(up(hidx_d, hidx.data(), sizeof(int32_t) * hidx.size()));
+    PLBA_CHECK(up(blk_r_d, blk_r.data(), sizeof(int32_t) * blk_r.size()));
+    PLBA_CHECK(up(blk_c_d, blk_c.data(), sizeof(int32_t) * blk_c.size()));
+    PLBA_CHECK(up(blk_off_d, blk_off.data(), sizeof(int32_t) * blk_off.size()));
+    PLBA_CHECK(up(blk_con_d, blk_con.data(), sizeof(int32_t) * blk_con.size()));
+    PLBA_CHECK(up(tf_d, tf.data(), sizeof(int32_t) * tf.size()));
+    PLBA_CHECK(up(tl_d, tl.data(), sizeof(int32_t) * tl.size()));
+    PLBA_CHECK(up(Zinv_d, Zi.data(), sizeof(double) * Zi.size()));
+    PLBA_CHECK(up(info_d, Om.data(), sizeof(double) * Om.size()));
+    PLBA_CHECK(up(T0, Tv.data(), sizeof(double) * Tv.size()));
+    PLBA_CHECK(hipMemsetAsync(P.x, 0, sizeof(double) * std::max(n, 1), s));  // g2o's _x starts at zero
+    PLBA_CHECK(hipMemsetAsync(ctrl_d, 0, sizeof(Ctrl), s));
+    P.nv = nv; P.ne = ne; P.nact = nact; P.nfree = nfree; P.n = n; P.nblk = nblk;
+    P.e_v = e_v_d; P.act = act_d; P.Zinv = Zinv_d; P.info = info_d; P.hidx = hidx_d;
+    P.T[0] = T0; P.T[1] = T1;
+    P.blk_r = blk_r_d; P.blk_c = blk_c_d; P.blk_off = blk_off_d; P.blk_con = blk_con_d;
+    dd.n = n; dd.ntiles = ntiles; dd.Ad = Ad; dd.bs = P.b; dd.xp = P.x; dd.ctrl = ctrl_d;
+    dd.tile_first = tf_d; dd.tile_last = tl_d;
+    double *hout = ctx->pgo_hout;
+    auto fetch = [&]() -> int {
+        PLBA_CHECK(hipMemcpyAsync(hout, P.out, sizeof(double) * 4, hipMemcpyDeviceToHost, s));
+        PLBA_CHECK(hipStreamSynchronize(s));
+        return PLBA_OK;
+    };
+    const int eb = std::max((nact + kPgoNT - 1) / kPgoNT, 1);
+    int cur = 0;
+    // computeActiveErrors() after the initial guess
+    hipLaunchKernelGGL(k_pgo_linearize<false>, dim3(eb), dim3(kPgoNT), 0, s, P, cur);
+    hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 0, 0.0);
+    PLBA_CHECK(hipGetLastError());
+    if (int rc = fetch()) return rc;
+    res->chi2_initial = hout[0];
+    res->n_free = nfree;
+    res->iterations = res->trials = res->solve_fails = 0;
+    res->n_trace = 0;
+    double lambda = 0.0, ni = 2.0, currentChi = hout[0];
+    for (int it = 0; it < prm.max_iters && nfree > 0; ++it) {
+        // OptimizationAlgorithmLevenberg::solve: computeActiveErrors, buildSystem
+        hipLaunchKernelGGL(k_pgo_linearize<true>, dim3(eb), dim3(kPgoNT), 0, s, P, cur);
+        hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 0, 0.0);
+        PLBA_CHECK(hipMemsetAsync(P.Hd, 0, sizeof(double) * (size_t)n * n, s));
+        hipLaunchKernelGGL(k_pgo_assemble, dim3((nblk * 42 + kPgoNT - 1) / kPgoNT), dim3(kPgoNT), 0, s, P);
+        if (it == 0 && prm.user_lambda_init <= 0.0) hipLaunchKernelGGL(k_pgo_maxdiag, dim3(1), dim3(64), 0, s, P);
+        PLBA_CHECK(hipGetLastError());
+        if (int rc = fetch()) return rc;
+        currentChi = hout[0];
+        const double chiStart = currentChi;
+        if (it == 0) {  // computeLambdaInit
+            lambda = prm.user_lambda_init > 0.0 ? prm.user_lambda_init : ctx->opts.tau * hout[2];
+            ni = 2.0;
+        }
+        const double lambdaStart = lambda;
+        double rho = 0.0;
+        int qmax = 0;
+        do {
+            // setLambda + solve (dense LDLᵀ, Cholmod's positive-definite test) + update
+            hipLaunchKernelGGL(k_pgo_damp, dim3((unsigned)(((size_t)n * n + 255) / 256)), dim3(256), 0, s, P, Ad, lambda);
+            for (int K = 0; K < ntiles; ++K) {
+                hipLaunchKernelGGL(k_dense_panel, dim3((ntiles - K + 1) / 2), dim3(kDensePanelNT), 0, s, dd, K);
+                const int m = ntiles - K - 1;
+                if (m > 0) hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, dd, K);
+            }
+            hipLaunchKernelGGL(k_pgo_check, dim3(1), dim3(256), 0, s, dd);
+            hipLaunchKernelGGL(k_pgo_solve, dim3(1), dim3(kFacThreads),
+                               n <= kSolveLdsN ? sizeof(double) * (size_t)n : 0, s, dd);
+            hipLaunchKernelGGL(k_pgo_update, dim3((nv + kPgoNT - 1) / kPgoNT), dim3(kPgoNT), 0, s, P, cur);
+            // restoreDiagonal (Hd is untouched), computeActiveErrors at the trial state
+            hipLaunchKernelGGL(k_pgo_linearize<false>, dim3(eb), dim3(kPgoNT), 0, s, P, cur ^ 1);
+            hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 1, lambda);
+            PLBA_CHECK(hipGetLastError());
+            if (int rc = fetch()) return rc;
+            const bool ok = hout[3] != 0.0;
+            double tempChi = hout[1];
+            if (!ok) {
+                tempChi = std::numeric_limits<double>::max();
+                ++res->solve_fails;
+            }
+            const double scale = hout[2] + 1e-3;
+            rho = (currentChi - tempChi) / scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                lambda *= std::max(1. / 3., alpha);
+                ni = 2;
+                currentChi = tempChi;
+                cur ^= 1;  // discardTop: the trial state becomes current
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                if (!std::isfinite(lambda)) break;  // (pop: the current state is untouched)
+            }
+            ++qmax;
+            ++res->trials;
+        } while (rho < 0 && qmax < prm.max_trials);
+        const int result = (qmax == prm.max_trials || rho == 0 || !std::isfinite(lambda)) ? 1 : 0;
+        if (res->trace && res->n_trace < res->trace_cap)
+            res->trace[res->n_trace++] = plba_iter_trace{0, it, qmax, result, chiStart, currentChi, lambdaStart, lambda};
+        ++res->iterations;
+        if (result != 0) break;
+    }
+    res->chi2_final = currentChi;
+    res->lambda_final = lambda;
+    if (res->v_T) {
+        PLBA_CHECK(hipMemcpyAsync(res->v_T, P.T[cur], sizeof(double) * 12 * (size_t)nv, hipMemcpyDeviceToHost, s));
+        PLBA_CHECK(hipStreamSynchronize(s));
+    }
+    res->solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return PLBA_OK;
 }
 

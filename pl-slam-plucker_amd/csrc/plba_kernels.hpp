@@ -1789,6 +1789,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d) {
 #include "plba_band_cl.hpp"
 #include "plba_bcr.hpp"
 #include "plba_dense.hpp"
+#include "plba_pgo.hpp"
 
 // ---------------------------------------------------------------- update + trial evaluation
 // stand-alone pose update (windows without free poses: no factorisation kernel to fuse into)

@@ -198,3 +198,58 @@ class HlmResultBuffers:
                     ln_line3d=self.ln_line3d,
                     linearizations=int(s.linearizations), solves=int(s.solves), accepted=int(s.accepted),
                     err=float(s.err), lam=float(s.lambda_), dx_norm=float(s.dx_norm), solve_ms=float(s.solve_ms))
+
+
+# ---- loop-closure pose graph (plba_pgo_*)
+class PlbaPgoGraph(C.Structure):
+    _fields_ = [("n_v", C.c_int32), ("n_e", C.c_int32), ("v_id", _ip), ("v_T", _dp), ("v_fixed", _bp),
+                ("e_v", _ip), ("e_Z", _dp), ("e_info", _dp)]
+
+
+class PlbaPgoParams(C.Structure):
+    _fields_ = [("user_lambda_init", C.c_double), ("max_iters", C.c_int32), ("initial_guess", C.c_int32),
+                ("max_trials", C.c_int32), ("pad", C.c_int32)]
+
+
+class PlbaPgoResult(C.Structure):
+    _fields_ = [("v_T", _dp), ("trace", C.POINTER(PlbaIterTrace)), ("trace_cap", C.c_int32), ("n_trace", C.c_int32),
+                ("iterations", C.c_int32), ("trials", C.c_int32), ("solve_fails", C.c_int32), ("n_free", C.c_int32),
+                ("chi2_initial", C.c_double), ("chi2_final", C.c_double), ("lambda_final", C.c_double),
+                ("solve_ms", C.c_double)]
+
+
+def pgo_params(**kw) -> PlbaPgoParams:
+    """plba_pgo_default_params: the reference's values (setUserLambdaInit(1e-10), maxItersPGO 100)."""
+    p = PlbaPgoParams(user_lambda_init=1e-10, max_iters=100, initial_guess=1, max_trials=10, pad=0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class PgoGraphView:
+    """Contiguous copies of a plba.pgo.PoseGraph's arrays and the PlbaPgoGraph over them."""
+
+    def __init__(self, pg):
+        self.v_id = np.ascontiguousarray(pg.v_id, dtype=np.int32)
+        self.v_T = np.ascontiguousarray(pg.v_T, dtype=np.float64).reshape(-1, 12)
+        self.v_fixed = np.ascontiguousarray(pg.v_fixed, dtype=np.uint8)
+        self.e_v = np.ascontiguousarray(pg.e_v, dtype=np.int32).reshape(-1, 2)
+        self.e_Z = np.ascontiguousarray(pg.e_Z, dtype=np.float64).reshape(-1, 12)
+        self.e_info = None if pg.e_info is None else np.ascontiguousarray(pg.e_info, dtype=np.float64).reshape(-1, 36)
+        self.struct = PlbaPgoGraph(
+            n_v=len(self.v_id), n_e=len(self.e_v), v_id=_ptr(self.v_id, _ip), v_T=_ptr(self.v_T, _dp),
+            v_fixed=_ptr(self.v_fixed, _bp), e_v=_ptr(self.e_v, _ip), e_Z=_ptr(self.e_Z, _dp),
+            e_info=_ptr(self.e_info, _dp) if self.e_info is not None else C.cast(None, _dp))
+
+
+class PgoResultBuffers:
+    def __init__(self, n_v: int, trace_cap: int = 256):
+        self.v_T = np.zeros((n_v, 12))
+        self.trace = (PlbaIterTrace * trace_cap)()
+        self.struct = PlbaPgoResult(v_T=_ptr(self.v_T, _dp), trace=self.trace, trace_cap=trace_cap)
+
+    def as_dict(self) -> dict:
+        s = self.struct
+        return dict(v_T=self.v_T.copy(), iterations=s.iterations, trials=s.trials, solve_fails=s.solve_fails,
+                    n_free=s.n_free, chi2_initial=s.chi2_initial, chi2_final=s.chi2_final,
+                    lambda_final=s.lambda_final, solve_ms=s.solve_ms, trace=trace_to_array(self.trace, s.n_trace))

@@ -28,6 +28,7 @@ EXPORTED = [
     "plba_synchronize", "plba_enable_kernel_timing", "plba_kernel_times", "plba_structure_stats",
     "plba_shard_plan", "plba_comm_unique_id", "plba_comm_init_rccl", "plba_comm_init_host",
     "plba_hlm_default_params", "plba_hlm_lba",
+    "plba_pgo_default_params", "plba_pgo_optimize",
 ]
 
 # int (*plba_host_allreduce_fn)(void *user, double *buf, int64_t n)
@@ -81,9 +82,13 @@ def load(path: Optional[str] = None):
     L.plba_hlm_default_params.restype = None
     L.plba_hlm_lba.argtypes = [vp, C.POINTER(capi.PlbaHlmState), C.POINTER(capi.PlbaHlmParams),
                                C.POINTER(capi.PlbaHlmResult)]
+    L.plba_pgo_default_params.argtypes = [C.POINTER(capi.PlbaPgoParams)]
+    L.plba_pgo_default_params.restype = None
+    L.plba_pgo_optimize.argtypes = [vp, C.POINTER(capi.PlbaPgoGraph), C.POINTER(capi.PlbaPgoParams),
+                                    C.POINTER(capi.PlbaPgoResult)]
     for name in EXPORTED:
         f = getattr(L, name)
-        if name not in ("plba_default_opts", "plba_last_error", "plba_hlm_default_params"):
+        if name not in ("plba_default_opts", "plba_last_error", "plba_hlm_default_params", "plba_pgo_default_params"):
             f.restype = C.c_int
     _lib = L
     return L
@@ -250,6 +255,19 @@ class Solver:
         if with_trace:
             out["trace"] = self.trace()
         return out
+
+    def pgo_optimize(self, pg, params=None) -> dict:
+        """Loop-closure pose graph (plba_pgo_optimize; src/mapHandler.cpp:5070-5531) of a
+        plba.pgo.PoseGraph: computeInitialGuess + optimize on this context's device. Needs no
+        uploaded window and leaves one intact."""
+        if params is None:
+            params = capi.PlbaPgoParams()
+            self.L.plba_pgo_default_params(C.byref(params))
+        gv = capi.PgoGraphView(pg)
+        rb = capi.PgoResultBuffers(len(gv.v_id))
+        self._check(self.L.plba_pgo_optimize(self.ctx, C.byref(gv.struct), C.byref(params), C.byref(rb.struct)),
+                    "plba_pgo_optimize")
+        return rb.as_dict()
 
     def trace(self) -> np.ndarray:
         n = C.c_int32(0)

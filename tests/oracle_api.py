@@ -30,8 +30,9 @@ _lib = None
 
 
 def build_oracle(force: bool = False) -> str:
-    src = os.path.join(ORACLE_DIR, "refcpu.cpp")
-    if force or not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+    srcs = [os.path.join(ORACLE_DIR, f) for f in ("refcpu.cpp", "refhlm.cpp", "refpgo.cpp", "refpgo.h")]
+    newest = max(os.path.getmtime(f) for f in srcs if os.path.exists(f))
+    if force or not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < newest:
         subprocess.run(["make", "-C", ORACLE_DIR, "-s"], check=True)
     return ORACLE_SO
 
@@ -209,3 +210,85 @@ def gba_line_obs(Tcw, P, Q, lo, cam, homog_th=1e-7):
     r, w, Jp, Jl = np.zeros(1), np.zeros(1), np.zeros(6), np.zeros(6)
     _hlm_lib().refhlm_gba_line_obs(*[_p(v) for v in a], *cam, homog_th, _p(r), _p(w), _p(Jp), _p(Jl))
     return r[0], w[0], Jp, Jl
+
+
+# ---- loop-closure pose graph oracle (oracle/refpgo.cpp)
+def _pgo_lib():
+    L = lib()
+    if not getattr(L, "_pgo_ready", False):
+        dp = C.POINTER(C.c_double)
+        L.refpgo_optimize.argtypes = [C.POINTER(capi.PlbaPgoGraph), C.POINTER(capi.PlbaPgoParams),
+                                      C.POINTER(capi.PlbaPgoResult)]
+        L.refpgo_optimize.restype = C.c_int
+        L.refpgo_initial_guess.argtypes = [C.POINTER(capi.PlbaPgoGraph), dp]
+        L.refpgo_quat_from_R.argtypes = [dp, dp]
+        L.refpgo_to_mqt.argtypes = [dp, dp]
+        L.refpgo_from_mqt.argtypes = [dp, dp]
+        L.refpgo_edge_error.argtypes = [dp, dp, dp, dp]
+        L.refpgo_edge_jacobians.argtypes = [dp, dp, dp, dp, dp]
+        L.refpgo_oplus.argtypes = [dp, dp, dp]
+        L._pgo_ready = True
+    return L
+
+
+def _f64(a, n=None):
+    return np.ascontiguousarray(a, dtype=np.float64).reshape(-1)
+
+
+def pgo_optimize(pg, params=None) -> dict:
+    """computeInitialGuess + optimize(max_iters) of a plba.pgo.PoseGraph."""
+    gv = capi.PgoGraphView(pg)
+    rb = capi.PgoResultBuffers(len(gv.v_id))
+    p = params if params is not None else capi.pgo_params()
+    rc = _pgo_lib().refpgo_optimize(C.byref(gv.struct), C.byref(p), C.byref(rb.struct))
+    assert rc == 0, rc
+    return rb.as_dict()
+
+
+def pgo_initial_guess(pg) -> np.ndarray:
+    gv = capi.PgoGraphView(pg)
+    out = np.zeros((len(gv.v_id), 12))
+    _pgo_lib().refpgo_initial_guess(C.byref(gv.struct), _p(out))
+    return out
+
+
+def quat_from_R(R):
+    R = _f64(R)
+    q = np.zeros(4)
+    _pgo_lib().refpgo_quat_from_R(_p(R), _p(q))
+    return q
+
+
+def to_mqt(T12):
+    T = _f64(T12)
+    v = np.zeros(6)
+    _pgo_lib().refpgo_to_mqt(_p(T), _p(v))
+    return v
+
+
+def from_mqt(v):
+    v = _f64(v)
+    T = np.zeros(12)
+    _pgo_lib().refpgo_from_mqt(_p(v), _p(T))
+    return T
+
+
+def se3_edge_error(Z, Xi, Xj):
+    Z, Xi, Xj = _f64(Z), _f64(Xi), _f64(Xj)
+    e = np.zeros(6)
+    _pgo_lib().refpgo_edge_error(_p(Z), _p(Xi), _p(Xj), _p(e))
+    return e
+
+
+def se3_edge_jacobians(Z, Xi, Xj):
+    Z, Xi, Xj = _f64(Z), _f64(Xi), _f64(Xj)
+    Ji, Jj = np.zeros(36), np.zeros(36)
+    _pgo_lib().refpgo_edge_jacobians(_p(Z), _p(Xi), _p(Xj), _p(Ji), _p(Jj))
+    return Ji.reshape(6, 6), Jj.reshape(6, 6)
+
+
+def se3_oplus(X, d):
+    X, d = _f64(X), _f64(d)
+    out = np.zeros(12)
+    _pgo_lib().refpgo_oplus(_p(X), _p(d), _p(out))
+    return out
