@@ -131,6 +131,31 @@ int plslam_get_point(plslam_map *m, int32_t idx, double xyz[3], int32_t *inlier,
 int plslam_get_line(plslam_map *m, int32_t idx, double NDw[6], int32_t *inlier, int32_t *local, int32_t *n_obs,
                     int32_t *kf_obs, double *obs, double *sigma, int32_t cap, uint8_t *med_desc);
 
+/* ---- loop-closure pose graph ----
+ * MapHandler::loopClosureOptimizationEssGraphG2O (src/mapHandler.cpp:5070-5299, ess = 1) and
+ * ::loopClosureOptimizationCovGraphG2O (:5301-5531, ess = 0): the g2o VertexSE3 / EdgeSE3 graph of
+ * the loop's KFs solved by plba_pgo_optimize (or the hook), then T_kf_w / x_kf_w of those KFs,
+ * their landmarks (point3D, med_obs_dir, dir_list; line3D, med_obs_dir, dir_list) and every
+ * later KF corrected, lc_idx_list[.][2] = 0, lc_state = LC_IDLE. loopClosureFuseLandmarks()
+ * (:5533, descriptor matching) is the caller's. lc_idxs / lc_idx_list: [n][3] int, lc_pose_list:
+ * [n][6] ([t; ω], include/mapHandler.h:186-187). */
+int plslam_set_loop_closure(plslam_map *m, int32_t n_lc_idxs, const int32_t *lc_idxs, int32_t n_lc_idx_list,
+                            const int32_t *lc_idx_list, int32_t n_lc_pose_list, const double *lc_pose_list);
+int plslam_get_lc_idx_list(plslam_map *m, int32_t *out, int32_t cap, int32_t *n);
+/* SlamConfig::minLMEssGraph (150) and maxItersPGO (100) (src/slamConfig.cpp:60,79) */
+int plslam_set_pgo_params(plslam_map *m, int32_t min_lm_ess_graph, int32_t max_iters_pgo);
+typedef int (*plslam_pgo_solve_fn)(void *user, const plba_pgo_graph *g, const plba_pgo_params *p,
+                                   plba_pgo_result *r);
+int plslam_set_pgo_solver(plslam_map *m, plslam_pgo_solve_fn fn, void *user);  /* NULL = plba_pgo_optimize */
+typedef struct plslam_pgo_stats {
+    int32_t kf_prev_idx, kf_curr_idx, n_vertices, n_fixed, n_edges, n_loop_edges, iterations, trials;
+    double  chi2_initial, chi2_final, solve_ms;
+} plslam_pgo_stats;
+int plslam_loop_closure_optimization(plslam_map *m, int32_t ess, plslam_pgo_stats *stats);
+/* MapLine::line3D / med_obs_dir (include/mapFeatures.h:93-94; never set in Plücker mode) */
+int plslam_set_line_geometry(plslam_map *m, int32_t idx, const double line3D[6], const double med_obs_dir[3]);
+int plslam_get_line_geometry(plslam_map *m, int32_t idx, double line3D[6], double med_obs_dir[3]);
+
 /* MapLine::changePlukerToOrth / changeOrthToPluker (src/mapFeatures.cpp:186-221) */
 void plslam_pluker_to_orth(const double NDw[6], double orth[4]);
 void plslam_orth_to_pluker(const double orth[4], double NDw[6]);

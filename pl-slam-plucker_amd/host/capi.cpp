@@ -232,6 +232,75 @@ int plslam_local_ba_plucker(plslam_map *m, plslam_hlm_stats *stats) {
     return PLBA_OK;
 }
 
+int plslam_set_loop_closure(plslam_map *m, int32_t n_lc_idxs, const int32_t *lc_idxs, int32_t n_lc_idx_list,
+                            const int32_t *lc_idx_list, int32_t n_lc_pose_list, const double *lc_pose_list) {
+    if (!m || n_lc_idxs < 0 || n_lc_idx_list < 0 || n_lc_pose_list < 0 || (n_lc_idxs && !lc_idxs) ||
+        (n_lc_idx_list && !lc_idx_list) || (n_lc_pose_list && !lc_pose_list))
+        return PLBA_E_INVALID;
+    MapHandler &mh = m->mh;
+    mh.lc_idxs.assign((size_t)n_lc_idxs, Vec3i{});
+    for (int i = 0; i < n_lc_idxs; ++i) mh.lc_idxs[i] = Vec3i{lc_idxs[3 * i], lc_idxs[3 * i + 1], lc_idxs[3 * i + 2]};
+    mh.lc_idx_list.assign((size_t)n_lc_idx_list, Vec3i{});
+    for (int i = 0; i < n_lc_idx_list; ++i)
+        mh.lc_idx_list[i] = Vec3i{lc_idx_list[3 * i], lc_idx_list[3 * i + 1], lc_idx_list[3 * i + 2]};
+    mh.lc_pose_list.assign((size_t)n_lc_pose_list, Vec6{});
+    for (int i = 0; i < n_lc_pose_list; ++i)
+        for (int k = 0; k < 6; ++k) mh.lc_pose_list[i][k] = lc_pose_list[6 * i + k];
+    return PLBA_OK;
+}
+
+int plslam_get_lc_idx_list(plslam_map *m, int32_t *out, int32_t cap, int32_t *n) {
+    if (!m) return PLBA_E_INVALID;
+    const auto &l = m->mh.lc_idx_list;
+    if (n) *n = (int32_t)l.size();
+    for (int i = 0; i < (int)l.size() && i < cap && out; ++i)
+        for (int k = 0; k < 3; ++k) out[3 * i + k] = l[i][k];
+    return PLBA_OK;
+}
+
+int plslam_set_pgo_params(plslam_map *m, int32_t min_lm_ess_graph, int32_t max_iters_pgo) {
+    if (!m || max_iters_pgo < 0) return PLBA_E_INVALID;
+    m->mh.params.min_lm_ess_graph = min_lm_ess_graph;
+    m->mh.params.max_iters_pgo = max_iters_pgo;
+    return PLBA_OK;
+}
+
+int plslam_set_pgo_solver(plslam_map *m, plslam_pgo_solve_fn fn, void *user) {
+    if (!m) return PLBA_E_INVALID;
+    m->mh.setPgoSolver(fn, user);
+    return PLBA_OK;
+}
+
+int plslam_loop_closure_optimization(plslam_map *m, int32_t ess, plslam_pgo_stats *stats) {
+    if (!m) return PLBA_E_INVALID;
+    PgoStats st;
+    const int rc = ess ? m->mh.loopClosureOptimizationEssGraphG2O(&st) : m->mh.loopClosureOptimizationCovGraphG2O(&st);
+    if (rc) return rc;
+    if (stats) {
+        stats->kf_prev_idx = st.kf_prev_idx; stats->kf_curr_idx = st.kf_curr_idx;
+        stats->n_vertices = st.n_vertices; stats->n_fixed = st.n_fixed; stats->n_edges = st.n_edges;
+        stats->n_loop_edges = st.n_loop_edges; stats->iterations = st.iterations; stats->trials = st.trials;
+        stats->chi2_initial = st.chi2_initial; stats->chi2_final = st.chi2_final; stats->solve_ms = st.solve_ms;
+    }
+    return PLBA_OK;
+}
+
+int plslam_set_line_geometry(plslam_map *m, int32_t idx, const double line3D[6], const double med_obs_dir[3]) {
+    if (!m || idx < 0 || idx >= (int)m->mh.map_lines.size() || !m->mh.map_lines[idx]) return PLBA_E_INVALID;
+    MapLine *ml = m->mh.map_lines[idx];
+    if (line3D) for (int k = 0; k < 6; ++k) ml->line3D[k] = line3D[k];
+    if (med_obs_dir) for (int k = 0; k < 3; ++k) ml->med_obs_dir[k] = med_obs_dir[k];
+    return PLBA_OK;
+}
+
+int plslam_get_line_geometry(plslam_map *m, int32_t idx, double line3D[6], double med_obs_dir[3]) {
+    if (!m || idx < 0 || idx >= (int)m->mh.map_lines.size() || !m->mh.map_lines[idx]) return PLBA_E_INVALID;
+    const MapLine *ml = m->mh.map_lines[idx];
+    if (line3D) for (int k = 0; k < 6; ++k) line3D[k] = ml->line3D[k];
+    if (med_obs_dir) for (int k = 0; k < 3; ++k) med_obs_dir[k] = ml->med_obs_dir[k];
+    return PLBA_OK;
+}
+
 int plslam_set_params(plslam_map *m, int32_t min_lm_obs, int32_t min_lm_cov_graph, int32_t min_kf_local_map) {
     if (!m) return PLBA_E_INVALID;
     m->mh.params.min_lm_obs = min_lm_obs;

@@ -694,7 +694,7 @@ int MapHandler::localBundleAdjustmentForPluker(HlmStats *stats) {
     g.pt_xyz = pt_xyz.data(); g.pt_id = pt_id.data(); g.ln_orth = ln_orth.data(); g.ln_id = ln_id.data();
     g.ept_lm = ept_lm.data(); g.ept_kf = ept_kf.data(); g.ept_obs = ept_obs.data(); g.ept_info = ept_info.data();
     g.eln_lm = eln_lm.data(); g.eln_kf = eln_kf.data(); g.eln_obs = eln_obs.data(); g.eln_info = eln_info.data();
-    plba_hlm_state hs{kf_x.data(), ln_plk.data()};
+    plba_hlm_state hs{kf_x.data(), ln_plk.data(), nullptr};
     std::vector<double> x_out(kf_x.size()), T_out(kf_Tcw.size()), xyz_out(pt_xyz.size()), orth_out(ln_orth.size());
     plba_hlm_result r{};
     r.kf_x = x_out.data(); r.kf_Tcw = T_out.data(); r.pt_xyz = xyz_out.data(); r.ln_orth = orth_out.data();

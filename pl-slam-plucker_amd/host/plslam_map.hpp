@@ -23,6 +23,7 @@ using Vec3 = std::array<double, 3>;
 using Vec4 = std::array<double, 4>;
 using Vec6 = std::array<double, 6>;
 using Mat4 = std::array<double, 16>;  // row-major
+using Vec3i = std::array<int, 3>;
 using Desc = std::vector<uint8_t>;
 
 // StVO::StereoFrame, reduced to what the LBA touches: the idx of each point / line feature
@@ -74,6 +75,12 @@ struct MapLine {
     std::vector<Vec4> NDw_obs_list;
     std::vector<int> kf_obs_list;
     std::vector<double> sigma_list;
+    // endpoint geometry (include/mapFeatures.h:93-100): not set by the Plücker constructor
+    // (src/mapFeatures.cpp:110-118, left uninitialised there, zero here); the loop-closure
+    // write-back transforms it (src/mapHandler.cpp:5224-5238)
+    Vec6 line3D{};
+    Vec3 med_obs_dir{};
+    std::vector<Vec3> dir_list;
 
     MapLine(int idx_, const Vec6 &NDw_, const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2);
     void addMapLineObservation(const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2);
@@ -127,6 +134,18 @@ struct SlamParams {
     int min_lm_obs = 5;         // SlamConfig::minLMObs()
     int min_lm_cov_graph = 75;  // SlamConfig::minLMCovGraph()
     int min_kf_local_map = 3;   // SlamConfig::minKFLocalMap()
+    int min_lm_ess_graph = 150; // SlamConfig::minLMEssGraph()  (src/slamConfig.cpp:60)
+    int max_iters_pgo = 100;    // SlamConfig::maxItersPGO()    (src/slamConfig.cpp:79)
+};
+
+using PgoSolveFn = int (*)(void *user, const plba_pgo_graph *g, const plba_pgo_params *p, plba_pgo_result *r);
+
+// One loopClosureOptimization{EssGraph,CovGraph}G2O call.
+struct PgoStats {
+    int kf_prev_idx = 0, kf_curr_idx = -1;
+    int n_vertices = 0, n_fixed = 0, n_edges = 0, n_loop_edges = 0;
+    int iterations = 0, trials = 0;
+    double chi2_initial = 0, chi2_final = 0, solve_ms = 0;
 };
 
 struct CullStats {
@@ -169,10 +188,23 @@ class MapHandler {
     // hand-rolled LM LBA of the Plücker map (dead code in the reference's localMappingThread,
     // :1277, kept callable). Returns PLBA_OK (stats->ret carries the reference's 0 / -1).
     int localBundleAdjustmentForPluker(HlmStats *stats = nullptr);
-    plba_hlm_params hlm_params{1e-5, 10.0, 1e-7, 1e-7, 1e-7, 15, 0};
+    plba_hlm_params hlm_params{1e-5, 10.0, 1e-7, 1e-7, 1e-7, 15, 0, PLBA_HLM_LBA_PLUCKER, 0};
     bool vo_inserting_kf = false;  // vo_status == VO_INSERTING_KF (:2160): nothing is written back
 
+    // src/mapHandler.cpp:5070-5299 / :5301-5531: the loop-closure pose graph (VertexSE3 per KF from
+    // the loop's first to its last KF, EdgeSE3 for covisible / consecutive pairs and for each
+    // loop), optimised on the GPU (plba_pgo_optimize), then the KF poses, their landmarks and
+    // every later KF corrected, lc_idx_list marked optimised, lc_state = LC_IDLE.
+    // loopClosureFuseLandmarks() (:5533, descriptor-matching landmark fusion) is the caller's.
+    int loopClosureOptimizationEssGraphG2O(PgoStats *stats = nullptr);
+    int loopClosureOptimizationCovGraphG2O(PgoStats *stats = nullptr);
+    // include/mapHandler.h:186-200
+    std::vector<Vec3i> lc_idxs, lc_idx_list;
+    std::vector<Vec6> lc_poses, lc_pose_list;
+    int lc_state = 0;  // LC_IDLE = 0
+
     void setSolver(SolveFn fn, void *user) { solve_fn_ = fn; solve_user_ = user; }
+    void setPgoSolver(PgoSolveFn fn, void *user) { pgo_fn_ = fn; pgo_user_ = user; }
     void setHlmSolver(HlmSolveFn fn, void *user) { hlm_fn_ = fn; hlm_user_ = user; }
     const std::string &lastError() const { return err_; }
     void setError(const char *fmt, ...);
@@ -194,6 +226,9 @@ class MapHandler {
     void *solve_user_ = nullptr;
     HlmSolveFn hlm_fn_ = nullptr;
     void *hlm_user_ = nullptr;
+    PgoSolveFn pgo_fn_ = nullptr;
+    void *pgo_user_ = nullptr;
+    int loopClosurePGO(bool ess, PgoStats *stats);
     std::string err_;
 };
 
@@ -201,6 +236,7 @@ class MapHandler {
 Mat4 inverse4(const Mat4 &T);  // Eigen Matrix4d::inverse (general cofactor inverse)
 // src2/auxiliar.cpp:113-173 (row-major 4x4, x = [t; ω])
 Mat4 inverse_se3(const Mat4 &T);
+Mat4 mul4(const Mat4 &A, const Mat4 &B);  // Matrix4d * Matrix4d
 Mat4 expmap_se3(const Vec6 &x);
 Vec6 logmap_se3(const Mat4 &T);
 int hamming(const Desc &a, const Desc &b);

@@ -110,3 +110,49 @@ def loop_graph(n_kf: int = 40, seed: int = 7, cov_window: int = 3, rot_noise_deg
             e_info[e] = (np.eye(6) + A @ A.T).reshape(36)
     return PoseGraph(np.arange(n_kf, dtype=np.int32), v_T, fixed, np.array(ev, np.int32), np.array(ez),
                      e_info, np.array([to12(M) for M in Tt]))
+
+
+def loop_map(n_loop: int = 24, n_after: int = 3, seed: int = 3, pts_per_kf: int = 3, lns_per_kf: int = 1):
+    """A SlamMap (plba.slam_map) whose keyframes drift around a loop of n_loop KFs (KF 0 ..
+    n_loop-1 closes on KF 0) followed by n_after KFs past the loop, with points / lines attached
+    to each KF (map_points_kf_idx / map_lines_kf_idx), a covisibility full_graph (>= 150 shared
+    landmarks for |i-j| <= 2) and the loop lists: lc_idxs = lc_idx_list = [(0, n_loop-1, 1)],
+    lc_pose_list = [logmap(T_true_j · T_true_0⁻¹)] so expmap(lc_pose)·T_kf_w(0) is the true pose of
+    the loop KF. Returns (SlamMap, lc_idxs, lc_idx_list, lc_pose_list, line3d[n_ln][6])."""
+    from . import geometry as geo
+    from .slam_map import DESC_BYTES, KF, Landmark, SlamMap
+    rng = np.random.default_rng(seed)
+    pg = loop_graph(n_kf=n_loop + n_after, seed=seed, ess=False)
+    n_kf = n_loop + n_after
+    Te = [to4(T) for T in pg.v_T]
+    Tt = [to4(T) for T in pg.T_true]
+    kfs, points, lines, mpk, mlk = [], [], [], {}, {}
+    line3d = []
+    for k in range(n_kf):
+        kfs.append(KF(k, Te[k].copy(), False, [], []))
+        mpk[k], mlk[k] = [], []
+        for _ in range(pts_per_kf):
+            idx = len(points)
+            pos = Te[k][:3, :3] @ rng.normal(0, 1, 3) + Te[k][:3, 3]
+            d = rng.normal(size=3)
+            points.append(Landmark(idx, False, True, pos, [rng.integers(0, 256, DESC_BYTES, dtype=np.uint8)],
+                                   [rng.normal(300, 50, 2)], [k], [1.0], [d / np.linalg.norm(d)]))
+            mpk[k].append(idx)
+        for _ in range(lns_per_kf):
+            idx = len(lines)
+            P, Q = rng.normal(0, 1, 3) + Te[k][:3, 3], rng.normal(0, 1, 3) + Te[k][:3, 3]
+            dv = (Q - P) / np.linalg.norm(Q - P)
+            lines.append(Landmark(idx, False, True, np.concatenate([np.cross(P, dv), dv]),
+                                  [rng.integers(0, 256, DESC_BYTES, dtype=np.uint8)], [rng.normal(0, 1, 4)], [k], [1.0]))
+            line3d.append(np.concatenate([P, Q]))
+            mlk[k].append(idx)
+    fg = np.zeros((n_kf, n_kf), np.uint32)
+    for i in range(n_kf):
+        for j in range(n_kf):
+            if i != j and abs(i - j) <= 2:
+                fg[i, j] = 200
+    m = SlamMap(458.654, 457.296, 367.215, 248.375, kfs, points, lines, mpk, fg, mlk, max_kf_idx=n_kf - 1)
+    lj = n_loop - 1
+    lc = np.array([[0, lj, 1]], np.int32)
+    x = geo.logmap_se3(Tt[lj] @ inv4(Tt[0]))
+    return m, lc.copy(), lc.copy(), np.array([x]), np.array(line3d)

@@ -190,6 +190,20 @@ HLM_SOLVE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(capi.PlbaGraph), C.POI
                            C.POINTER(capi.PlbaHlmParams), C.POINTER(capi.PlbaHlmResult))
 
 
+PGO_SOLVE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(capi.PlbaPgoGraph), C.POINTER(capi.PlbaPgoParams),
+                           C.POINTER(capi.PlbaPgoResult))
+
+
+class PlslamPgoStats(C.Structure):
+    _fields_ = [("kf_prev_idx", C.c_int32), ("kf_curr_idx", C.c_int32), ("n_vertices", C.c_int32),
+                ("n_fixed", C.c_int32), ("n_edges", C.c_int32), ("n_loop_edges", C.c_int32),
+                ("iterations", C.c_int32), ("trials", C.c_int32),
+                ("chi2_initial", C.c_double), ("chi2_final", C.c_double), ("solve_ms", C.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 class PlslamHlmStats(C.Structure):
     _fields_ = [("ret", C.c_int32), ("n_kf_list", C.c_int32), ("n_fixed_kf", C.c_int32), ("n_pt", C.c_int32),
                 ("n_ln", C.c_int32), ("n_pt_obs", C.c_int32), ("n_ls_obs", C.c_int32),
@@ -211,6 +225,8 @@ HOST_EXPORTED = [
     "plslam_form_local_map", "plslam_remove_bad_landmarks_pluker", "plslam_local_mapping_step", "plslam_exists",
     "plslam_set_keyframe_x", "plslam_get_keyframe_x", "plslam_set_hlm_solver", "plslam_set_hlm_params",
     "plslam_local_ba_plucker",
+    "plslam_set_loop_closure", "plslam_get_lc_idx_list", "plslam_set_pgo_params", "plslam_set_pgo_solver",
+    "plslam_loop_closure_optimization", "plslam_set_line_geometry", "plslam_get_line_geometry",
 ]
 
 
@@ -272,6 +288,13 @@ def load_host(path: Optional[str] = None):
     L.plslam_set_hlm_solver.argtypes = [vp, HLM_SOLVE_FN, vp]
     L.plslam_set_hlm_params.argtypes = [vp, C.POINTER(capi.PlbaHlmParams), C.c_int32]
     L.plslam_local_ba_plucker.argtypes = [vp, C.POINTER(PlslamHlmStats)]
+    L.plslam_set_loop_closure.argtypes = [vp, C.c_int32, ip, C.c_int32, ip, C.c_int32, dp]
+    L.plslam_get_lc_idx_list.argtypes = [vp, ip, C.c_int32, ip]
+    L.plslam_set_pgo_params.argtypes = [vp, C.c_int32, C.c_int32]
+    L.plslam_set_pgo_solver.argtypes = [vp, PGO_SOLVE_FN, vp]
+    L.plslam_loop_closure_optimization.argtypes = [vp, C.c_int32, C.POINTER(PlslamPgoStats)]
+    L.plslam_set_line_geometry.argtypes = [vp, C.c_int32, dp, dp]
+    L.plslam_get_line_geometry.argtypes = [vp, C.c_int32, dp, dp]
     for n in HOST_EXPORTED:
         if n not in ("plslam_map_last_error", "plslam_pluker_to_orth", "plslam_orth_to_pluker"):
             getattr(L, n).restype = C.c_int
@@ -421,6 +444,59 @@ class HostMap:
         st = PlslamHlmStats()
         self._check(self.L.plslam_local_ba_plucker(self.h, C.byref(st)), "local_ba_plucker")
         return st.as_dict()
+
+    # ---- loop-closure pose graph (src/mapHandler.cpp:5070-5531)
+    def set_loop_closure(self, lc_idxs, lc_idx_list, lc_pose_list):
+        a = np.ascontiguousarray(np.asarray(lc_idxs, np.int32).reshape(-1, 3))
+        b = np.ascontiguousarray(np.asarray(lc_idx_list, np.int32).reshape(-1, 3))
+        c = np.ascontiguousarray(np.asarray(lc_pose_list, np.float64).reshape(-1, 6))
+        ip = C.POINTER(C.c_int32)
+        self._check(self.L.plslam_set_loop_closure(self.h, len(a), a.ctypes.data_as(ip), len(b), b.ctypes.data_as(ip),
+                                                   len(c), c.ctypes.data_as(C.POINTER(C.c_double))), "set_loop_closure")
+
+    def lc_idx_list(self) -> np.ndarray:
+        n = C.c_int32(0)
+        self._check(self.L.plslam_get_lc_idx_list(self.h, None, 0, C.byref(n)), "get_lc_idx_list")
+        out = np.zeros((max(n.value, 1), 3), np.int32)
+        self._check(self.L.plslam_get_lc_idx_list(self.h, out.ctypes.data_as(C.POINTER(C.c_int32)), n.value,
+                                                  C.byref(n)), "get_lc_idx_list")
+        return out[:n.value]
+
+    def set_pgo_params(self, min_lm_ess_graph: int = 150, max_iters_pgo: int = 100):
+        self._check(self.L.plslam_set_pgo_params(self.h, min_lm_ess_graph, max_iters_pgo), "set_pgo_params")
+
+    def set_pgo_solver(self, fn: Optional[Callable]):
+        """fn(graph, params, result) -> int, or None for the MI355X backend (plba_pgo_optimize)."""
+        if fn is None:
+            self._pcb = None
+            self._check(self.L.plslam_set_pgo_solver(self.h, C.cast(None, PGO_SOLVE_FN), None), "set_pgo_solver")
+            return
+
+        def tramp(user, gp, pp, rp):
+            try:
+                return int(fn(gp.contents, pp.contents, rp.contents))
+            except Exception:  # never unwind through C
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._pcb = PGO_SOLVE_FN(tramp)
+        self._check(self.L.plslam_set_pgo_solver(self.h, self._pcb, None), "set_pgo_solver")
+
+    def loop_closure(self, ess: bool = True) -> dict:
+        st = PlslamPgoStats()
+        self._check(self.L.plslam_loop_closure_optimization(self.h, int(ess), C.byref(st)), "loop_closure")
+        return st.as_dict()
+
+    def set_line_geometry(self, idx: int, line3d, med_obs_dir):
+        a, pa = _d(line3d)
+        b, pb = _d(med_obs_dir)
+        self._check(self.L.plslam_set_line_geometry(self.h, idx, pa, pb), "set_line_geometry")
+
+    def line_geometry(self, idx: int):
+        a, b = np.zeros(6), np.zeros(3)
+        self._check(self.L.plslam_get_line_geometry(self.h, idx, a.ctypes.data_as(C.POINTER(C.c_double)),
+                                                    b.ctypes.data_as(C.POINTER(C.c_double))), "get_line_geometry")
+        return a, b
 
     def keyframe_x(self, kf_idx: int) -> np.ndarray:
         x = np.zeros(6)
