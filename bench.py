@@ -10,10 +10,12 @@ configs[2], the window north_star quotes its ≥50x target on).
 
 Multi-GPU (`--gpus N`, launched by torch.distributed.run), two modes:
   --mode shard (default for N > 1)  ONE window split over the ranks by landmark:
-                             BASELINE.json configs[3] (C4, 400 KF, "sharded 4×MI355X") for N = 2, 4
-                             and configs[4] (C5, 1000 KF, 8×MI355X) for N = 8; partial reduced
+                             BASELINE.json configs[4] (C5, 1000 KF, "report 1/2/4/8 scaling")
+                             for every N > 1 (`--config C4` gives configs[3]); partial reduced
                              camera systems summed with RCCL all-reduces inside the captured step
-                             graph (strong scaling); `--transport host` rehearses it with gloo.
+                             graph (strong scaling); rank 0 also times the same window unsharded on
+                             its GPU ("scaling_reference", the curve's 1-GPU point);
+                             `--transport host` rehearses it with gloo.
   --mode replicas            every rank solves its own independent C3 window (different seed):
                              independent LBA windows need no data-path collective (weak scaling).
 The barrier and max-over-ranks timing use torch.distributed in both.
@@ -54,7 +56,7 @@ def parse():
     p.add_argument("--cpu-runs", type=int, default=5)
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK (multi-rank rehearsal on 1 GPU)")
     p.add_argument("--mode", choices=["replicas", "shard"], default=None,
-                   help="default: replicas at N=1 (one C3 window), shard for N>1")
+                   help="default: replicas at N=1 (one C3 window), shard (C5) for N>1")
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="--mode shard all-reduce transport")
     return p.parse_args()
 
@@ -118,7 +120,10 @@ def main():
         a.mode = "shard" if world > 1 else "replicas"
     shard = a.mode == "shard"
     if shard and "--config" not in sys.argv:
-        a.config = "C5" if world >= 8 else "C4"   # BASELINE.json configs[4] / configs[3]
+        # BASELINE.json configs[4]: the 1000-KF window, "report 1/2/4/8 scaling" — every N > 1
+        # shards the same C5 window, so the N = 2, 4, 8 points form one strong-scaling curve
+        # (its one-GPU point is measured in the same job: "scaling_reference")
+        a.config = "C5"
     base_seed = synth.CONFIGS[a.config][3]
     dev = local if a.device is None else a.device
     if shard:  # one window for all ranks
@@ -196,6 +201,31 @@ def main():
         t2 = time.perf_counter()
         e2e.append(dict(end_to_end_ms=(t2 - t0) * 1e3, upload_ms=(t1 - t0) * 1e3,
                         solve_and_download_ms=(t2 - t1) * 1e3, solve_ms=float(r2["solve_ms"])))
+
+    # the same window unsharded on one GPU (rank 0, outside the timed region): the N = 1 point of
+    # the sharded strong-scaling curve
+    scaling_ref = None
+    if shard and world > 1:
+        if rank == 0:
+            ref = Solver(device=dev)
+            ref.upload(g)
+            for _ in range(max(a.warmup, 1)):
+                ref.reset()
+                ref.lba_plucker(want_outputs=False, with_trace=False)
+            ref.synchronize()
+            t0 = time.perf_counter()
+            ri = 0
+            for _ in range(a.steps):
+                ref.reset()
+                rr = ref.lba_plucker(want_outputs=False, with_trace=False)
+                ri += int(rr["iters"][0] + rr["iters"][1])
+            ref.synchronize()
+            rdt = time.perf_counter() - t0
+            ref.close()
+            scaling_ref = {"config": a.config, "n_gpus": 1, "mode": "the same window, unsharded, one GPU",
+                           "value": ri / rdt, "unit": "LM iterations/s", "steps": a.steps,
+                           "speedup_of_this_run": (tot_iters / dt) / (ri / rdt)}
+        dist.barrier()
 
     if rank == 0:
         # dominant kernel by device time in the instrumented step
@@ -280,6 +310,8 @@ def main():
             "kernels": per_kernel,
         }
         out["final_chi2_gpu"] = [float(r["chi2"][0]), float(r["chi2"][1])]
+        if scaling_ref is not None:
+            out["scaling_reference"] = scaling_ref
         if world == 1 and not a.no_cpu_baseline:
             try:
                 cb = cpu_baseline(a.config, a.cpu_runs if a.config in ("C1", "C1L", "C2", "C3") else 1)
