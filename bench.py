@@ -191,7 +191,8 @@ def main():
     # first pays one-time arena / code-object costs). Outside the timed region.
     e2e = []
     for k in range(2):
-        g2 = synth.generate(a.config, seed=base_seed + 7919 * (k + 1) + 97 * rank)
+        # (sharded: every rank uploads the same window — each keeps its landmark share)
+        g2 = synth.generate(a.config, seed=base_seed + 7919 * (k + 1) + (0 if shard else 97 * rank))
         if dist is not None:
             dist.barrier()
         t0 = time.perf_counter()
