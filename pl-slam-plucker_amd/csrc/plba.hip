@@ -894,6 +894,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ZALLOC(d.bcr_ctl, 4);
         ZALLOC(d.bcr_stamps, (size_t)d.bcr_N * kBcrStamps);
     }
+    if (!band_mode) ZALLOC(d.bcr_stamps, kBcrStamps);  // dense-path phase stamps (PLBA_DIAG bit 8)
     ALLOC(d.bs, n);
     ZALLOC(d.xp, n);
     ALLOC(d.Wbuf, (size_t)std::max(n, 1) * kTile);
@@ -1632,9 +1633,10 @@ int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [17][8] */) {
 // reduction launch, [bcr_rows][32] s_memrealtime ticks (100 MHz).
 int plba_debug_bcr_stamps(plba_ctx *ctx, unsigned long long *out, int32_t cap, int32_t *rows) {
     if (!ctx || !out || !rows) return PLBA_E_INVALID;
-    if (!ctx->uploaded || !ctx->d.bcr) return PLBA_E_STATE;
-    const int n = std::min(cap / kBcrStamps, ctx->d.bcr_N);
-    *rows = ctx->d.bcr_N;
+    if (!ctx->uploaded || !ctx->d.bcr_stamps) return PLBA_E_STATE;  // BCR rows, or 1 row (dense path)
+    const int rows_ = std::max(ctx->d.bcr_N, 1);
+    const int n = std::min(cap / kBcrStamps, rows_);
+    *rows = rows_;
     PLBA_CHECK(hipMemcpy(out, ctx->d.bcr_stamps, sizeof(unsigned long long) * (size_t)n * kBcrStamps, hipMemcpyDeviceToHost));
     return PLBA_OK;
 }

@@ -5,7 +5,7 @@
 // `Ad`, lower triangle) as a right-looking blocked LDLᵀ with 32×32 tiles, two launches per
 // panel K (captured in the step graph like every other kernel):
 //   k_dense_panel<K>   one wave per two row tiles I >= K: LDLᵀ of the diagonal tile S_KK in
-//                      registers (every workgroup redundantly — cheaper than a third launch),
+//                      LDS (every workgroup redundantly — cheaper than a third launch),
 //                      then W_IK = S_IK·L_KK⁻ᵀ (= L_IK·D_K) and L_IK = W_IK·D_K⁻¹ (I > K);
 //   k_dense_update<K>  one wave per trailing tile (I, J), K < J <= I: S_IJ -= W_IK·L_JKᵀ with
 //                      v_mfma_f64_16x16x4_f64 (2×2 blocks of 16×16, eight k-steps of 4), W and
@@ -18,8 +18,14 @@
 // B lane l -> B[k=l>>4][l&15]; C/D (f64 form) reg i -> row (l>>4)+4i, col l&15.
 #pragma once
 
-constexpr int kDT = 32;          // tile
+constexpr int kDT = 32;            // tile
 constexpr int kDensePanelNT = 64;  // one wave: two row tiles per workgroup
+// PLBA_DIAG bit 8 (diagnostics only): phase timestamps of panel / update K = 5, workgroup 0
+#define DENSE_STAMP(slot)                                                                                   \
+    do {                                                                                                   \
+        if ((d.diag & 8) && K == 5 && blockIdx.x == ((slot) < 8 ? 1u : 0u) && threadIdx.x == 0)           \
+            d.bcr_stamps[slot] = __builtin_amdgcn_s_memrealtime();                                        \
+    } while (0)
 
 // One wave per pair of row tiles (I0 = K + 2·blockIdx.x, I1 = I0 + 1), everything in registers:
 // lane l holds row l&31 of the diagonal tile S_KK and factorises it (every workgroup
@@ -29,7 +35,9 @@ constexpr int kDensePanelNT = 64;  // one wave: two row tiles per workgroup
 // arrays need compile-time indices; no LDS, no barriers.
 __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
     TRIAL_GUARD
+    DENSE_STAMP(0);
     if (K > 0 && d.ctrl->solve_ok == 0) return;  // an earlier panel hit a zero pivot
+    DENSE_STAMP(1);
     const int lane = threadIdx.x, r = lane & 31, n = d.n;
     const int k0 = K * kDT, kb = min(kDT, n - k0);
     const int I = K + 2 * (int)blockIdx.x + (lane >> 5);
@@ -45,6 +53,7 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
 #pragma unroll
     for (int c = 0; c < kDT; ++c)  // row r, lower part; rows past kb are identity rows
         t[c] = (r < kb && c <= r) ? t[c] : (c == r ? 1.0 : 0.0);
+    DENSE_STAMP(2);
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < kDT; ++j) {
@@ -57,6 +66,7 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
             if (r >= c) t[c] -= lrj * tcj;
         }
     }
+    DENSE_STAMP(3);
     // t[p] (p < r) = L[r][p]·D_p -> L[r][p]; t[r] = D_r
     double D[kDT];
 #pragma unroll
@@ -72,6 +82,7 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
                 if (c <= r) Ad[(size_t)(k0 + r) + (size_t)(k0 + c) * n] = t[c];
         }
     }
+    DENSE_STAMP(4);
     if (!ok || I == K || I >= d.ntiles) return;
     const bool live = i0 + r < n;
     double a[kDT];
@@ -86,13 +97,16 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
     for (int c = 1; c < kDT; ++c)
 #pragma unroll
         for (int p = 0; p < c; ++p) a[c] -= a[p] * readlane_f64(t[p], c);  // L[c][p]
+    DENSE_STAMP(5);  // (the compiler sinks part of the solve past this stamp)
     if (!live) return;
+    // W_IK = L_IK·D_K into Wbuf column-major ([kTile][n]: a lane per row, coalesced) and L_IK
 #pragma unroll
     for (int c = 0; c < kDT; ++c)
         if (c < kb) {
-            d.Wbuf[(size_t)(i0 + r) * kTile + c] = a[c];                     // W_IK = L_IK·D_K (row-major)
-            Ad[(size_t)(i0 + r) + (size_t)(k0 + c) * n] = a[c] / D[c];       // L_IK
+            d.Wbuf[(size_t)c * n + i0 + r] = a[c];
+            Ad[(size_t)(i0 + r) + (size_t)(k0 + c) * n] = a[c] / D[c];
         }
+    DENSE_STAMP(6);
 }
 
 // trailing tile index t -> (I, J) with K < J <= I < nt, row-major over the lower triangle
@@ -107,6 +121,7 @@ __device__ __forceinline__ void dense_tile_of(int t, int K, int &I, int &J) {
 
 __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
     TRIAL_GUARD
+    DENSE_STAMP(8);
     if (d.ctrl->solve_ok == 0) return;
     __shared__ double Ws[kDT][kDT + 1];  // W_IK rows
     __shared__ double Ls[kDT][kDT + 1];  // L_JK rows
@@ -116,14 +131,25 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
     const int k0 = K * kDT, kb = min(kDT, n - k0);
     const int i0 = I * kDT, j0 = J * kDT;
     const double *Ad = d.Ad;
-    // stage: W rows (row-major Wbuf, coalesced along p) and L_JK (column-major Ad, coalesced along rows)
-    for (int e = lane; e < kDT * kDT; e += 64) {
-        const int rr = e / kDT, p = e % kDT;
-        Ws[rr][p] = (i0 + rr < n && p < kb) ? d.Wbuf[(size_t)(i0 + rr) * kTile + p] : 0.0;
-        const int pc = e / kDT, jr = e % kDT;
-        Ls[jr][pc] = (j0 + jr < n && pc < kb) ? Ad[(size_t)(j0 + jr) + (size_t)(k0 + pc) * n] : 0.0;
+    // stage W_IK (column-major Wbuf) and L_JK (column-major Ad) through LDS: all loads issued
+    // first (clamped valid addresses, masked after)
+    constexpr int NU = kDT * kDT / 64;
+    double wv[NU], lv[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int e = lane + 64 * u, rr = e / kDT, p = e % kDT;  // W: (row rr, col p); L: (row p, col rr)
+        // (row index e % kDT along the lanes: both sources are column-major, coalesced)
+        wv[u] = d.Wbuf[(size_t)min(rr, kb - 1) * n + min(i0 + p, n - 1)];  // W[i0 + p][rr]
+        lv[u] = Ad[(size_t)min(j0 + p, n - 1) + (size_t)(k0 + min(rr, kb - 1)) * n];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int e = lane + 64 * u, rr = e / kDT, p = e % kDT;
+        Ws[p][rr] = (i0 + p < n && rr < kb) ? wv[u] : 0.0;
+        Ls[p][rr] = (j0 + p < n && rr < kb) ? lv[u] : 0.0;
     }
     __syncthreads();
+    DENSE_STAMP(9);
     dbl4 acc[2][2];
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
@@ -140,7 +166,9 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
         acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
         acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
     }
+    DENSE_STAMP(10);
     double *Aw = d.Ad;
+    double cv[2][2][4];  // the 16 entries of C this lane updates: all loads, then all stores
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -148,7 +176,16 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = i0 + 16 * bi + lk + 4 * i, col = j0 + 16 * bj + lr;
-                if (row < n && col < n && col <= row) Aw[(size_t)row + (size_t)col * n] -= acc[bi][bj][i];
+                cv[bi][bj][i] = Aw[(size_t)min(row, n - 1) + (size_t)min(col, n - 1) * n];
+            }
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = i0 + 16 * bi + lk + 4 * i, col = j0 + 16 * bj + lr;
+                if (row < n && col < n && col <= row) Aw[(size_t)row + (size_t)col * n] = cv[bi][bj][i] - acc[bi][bj][i];
             }
 }
 
