@@ -897,7 +897,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     if (!band_mode) ZALLOC(d.bcr_stamps, kBcrStamps);  // dense-path phase stamps (PLBA_DIAG bit 8)
     ALLOC(d.bs, n);
     ZALLOC(d.xp, n);
-    ALLOC(d.Wbuf, (size_t)std::max(n, 1) * kTile);
+    ALLOC(d.Wbuf, (size_t)std::max(n, 1) * (kTile + 1));  // W panel + y of the dense path
     UPLOAD(d.tile_first, tile_first);
     UPLOAD(d.tile_last, tile_last);
     ALLOC(d.part_chi2, d.n_lin_blocks);
@@ -1929,7 +1929,7 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
         {(void **)&P.eg, sizeof(double) * 12 * (size_t)ne}, {(void **)&P.echi, sizeof(double) * (size_t)ne},
         {(void **)&P.Hd, sizeof(double) * (size_t)n * n}, {(void **)&Ad, sizeof(double) * (size_t)n * n},
         {(void **)&P.b, sizeof(double) * (size_t)n}, {(void **)&P.x, sizeof(double) * (size_t)n},
-        {(void **)&dd.Wbuf, sizeof(double) * (size_t)std::max(n, 1) * kTile}, {(void **)&P.out, sizeof(double) * 4},
+        {(void **)&dd.Wbuf, sizeof(double) * (size_t)std::max(n, 1) * (kTile + 1)}, {(void **)&P.out, sizeof(double) * 4},
         {(void **)&ctrl_d, sizeof(Ctrl)}};
     size_t tot = 0;
     for (auto &sl : slots) tot += (std::max(sl.bytes, (size_t)128) + 255) & ~(size_t)255;

@@ -10,7 +10,9 @@
 //   k_dense_update<K>  one wave per trailing tile (I, J), K < J <= I: S_IJ -= W_IK·L_JKᵀ with
 //                      v_mfma_f64_16x16x4_f64 (2×2 blocks of 16×16, eight k-steps of 4), W and
 //                      L staged through LDS with coalesced loads.
-// Then k_dense_solve: forward / backward substitution through the factor (one workgroup,
+// The forward substitution L y = b rides along: panel K solves y_K = L_KK⁻¹ b_K on its diagonal
+// tile and the diagonal update tile (I, I) of step K subtracts L_IK·y_K from b_I (dense_yd).
+// Then k_dense_solve: D⁻¹ and the backward substitution through the factor (one workgroup,
 // envelope-aware) and the pose update — the tail of the single-workgroup k_rcs_factor.
 // Semantics of LinearSolverEigen (SimplicialLDLT): the solve fails iff a pivot is exactly 0;
 // later panels then skip their work and x_p keeps its previous value (A13).
@@ -80,6 +82,16 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
 #pragma unroll
             for (int c = 0; c < kDT; ++c)
                 if (c <= r) Ad[(size_t)(k0 + r) + (size_t)(k0 + c) * n] = t[c];
+        }
+        if (ok && lane < 32) {  // forward substitution of tile K: y_K = L_KK⁻¹ b_K
+            double *yd = dense_yd(d);
+            double yi = (K == 0 ? d.bs : yd)[k0 + min(r, kb - 1)];
+#pragma unroll
+            for (int j = 0; j < kDT; ++j) {
+                const double yj = readlane_f64(yi, j);
+                if (r > j && r < kb) yi -= t[j] * yj;
+            }
+            if (r < kb) yd[k0 + r] = yi;
         }
     }
     DENSE_STAMP(4);
@@ -167,6 +179,19 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
         acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
     }
     DENSE_STAMP(10);
+    if (I == J && lane < kDT && i0 + lane < n) {
+        // forward substitution of rows I against tile K: y_I -= L_IK·y_K (Ls holds L_IK here),
+        // summed in column order like the single-workgroup solve
+        double *yd = dense_yd(d);
+        double yk[kDT];
+#pragma unroll
+        for (int p = 0; p < kDT; ++p) yk[p] = yd[k0 + min(p, kb - 1)];
+        double s = 0.0;
+#pragma unroll
+        for (int p = 0; p < kDT; ++p)
+            if (p < kb) s += Ls[lane][p] * yk[p];
+        yd[i0 + lane] = (K == 0 ? d.bs : yd)[i0 + lane] - s;
+    }
     double *Aw = d.Ad;
     double cv[2][2][4];  // the 16 entries of C this lane updates: all loads, then all stores
 #pragma unroll
@@ -192,10 +217,13 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
 // forward / backward substitution through the dense factor + pose update (one workgroup)
 __global__ __launch_bounds__(kFacThreads) void k_dense_solve(Dev d) {
     TRIAL_GUARD
-    if (d.ctrl->solve_ok) {
-        if (d.n <= kSolveLdsN) dense_solve_wg<true>(d);
-        else dense_solve_wg<false>(d);
+    SOLVE_STAMP(12);
+    if (d.ctrl->solve_ok) {  // forward substitution done by the panels / updates (dense_yd)
+        if (d.n <= kSolveLdsN) dense_solve_wg<true, true>(d);
+        else dense_solve_wg<false, true>(d);
     }
     __syncthreads();
+    SOLVE_STAMP(14);
     pose_update_wg<kFacThreads>(d);  // applied even after a failed solve, with the previous x_p (A13)
+    SOLVE_STAMP(15);
 }

@@ -114,7 +114,7 @@ struct Dev {
     int32_t *ch_blk, *ch_off;           // [nch], [nch+1] (triple range)
     int32_t *blk_ch;                    // [nblk+1] chunk range of each block
     double *ch_part;                    // [nch][42]  partial block sums (36) + b_s sums (6)
-    double *Ad, *bs, *xp, *Wbuf;        // [n*n], [n], [n], [n*kTile]
+    double *Ad, *bs, *xp, *Wbuf;        // [n*n], [n], [n], [n*(kTile+1)] (W, then y of the dense path)
     int32_t *tile_first;                // [ntiles] first nonzero column tile of each row tile
     int32_t *tile_last;                 // [ntiles] last row tile whose envelope reaches column tile K
     // block-band storage (used when the envelope bandwidth bw <= kBandMax)
@@ -961,29 +961,45 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
 
 constexpr int kFacThreads = 1024;
 constexpr int kSolveLdsN = 6144;  // y held in (dynamic) LDS up to this n (48 KiB), in Wbuf beyond
+constexpr int kSolveTilesLds = 256;  // tile_first staged in LDS for the first 256 tiles
+// PLBA_DIAG bit 8 (diagnostics only): phase timestamps of the dense solve (slots 12-15)
+#define SOLVE_STAMP(slot)                                                                         \
+    do {                                                                                         \
+        if ((d.diag & 8) && d.bcr_stamps && blockIdx.x == 0 && threadIdx.x == 0)                 \
+            d.bcr_stamps[slot] = __builtin_amdgcn_s_memrealtime();                              \
+    } while (0)
 // ---- solve L D Lᵀ x = b_s through the envelope-aware dense factor in Ad (unit L below the
 // diagonal, D on it), tile by tile; one workgroup of kFacThreads. x -> xp.
 // Forward: wave 0 solves the diagonal tile (its row of L in registers, y_j broadcast by
 // readlane) while the other waves prefetch their rows' coefficients of the tile's columns
 // (independent of y); then those rows are updated. Backward: 32 partial column sums per tile
 // (lanes along rows), then wave 0 adds them and solves the tile. y lives in LDS (LY).
-template <bool LY>
+// y of the dense path's fused forward substitution: behind the W panel in Wbuf
+__device__ __forceinline__ double *dense_yd(const Dev &d) { return d.Wbuf + (size_t)kTile * d.n; }
+
+// FWD: y = L⁻¹b already in dense_yd (the MFMA factorisation did the forward substitution)
+template <bool LY, bool FWD = false>
 __device__ __forceinline__ void dense_solve_wg(const Dev &d) {
     extern __shared__ double y_lds[];
     __shared__ double red[kFacThreads / kTile][kTile + 1];
+    __shared__ int tfs[kSolveTilesLds];  // tile_first in LDS (the envelope tests of every row)
     const int tid = threadIdx.x;
     const int n = d.n;
     const int nt = d.ntiles;
     const double *Ad = d.Ad;
     double *y = LY ? y_lds : d.Wbuf;
-    for (int i = tid; i < n; i += kFacThreads) y[i] = d.bs[i];
+    const double *y0 = FWD ? dense_yd(d) : d.bs;
+    for (int i = tid; i < n; i += kFacThreads) y[i] = y0[i];
+    for (int t = tid; t < kSolveTilesLds; t += kFacThreads) tfs[t] = t < nt ? d.tile_first[t] : 0;
+    auto tile_first = [&](int t) { return t < kSolveTilesLds ? tfs[t] : d.tile_first[t]; };
     __syncthreads();
     constexpr int kRowThreads = kFacThreads - 64;
-    for (int K = 0; K < nt; ++K) {
+    for (int K = 0; K < (FWD ? 0 : nt); ++K) {
         const int k0 = K * kTile, kb = min(kTile, n - k0);
         const int fend = min(n, (d.tile_last[K] + 1) * kTile);
         const int i1 = k0 + kb + tid - 64;  // this thread's first row of the update
         double cf[kTile];
+        if (K == 5) SOLVE_STAMP(16);
         if (tid < 64) {
             double yi = (tid < kb) ? y[k0 + tid] : 0.0;
             // loads at clamped (always valid) addresses, selected after: no per-element branches
@@ -997,14 +1013,16 @@ __device__ __forceinline__ void dense_solve_wg(const Dev &d) {
                 if (tid > j && tid < kb) yi -= l[j] * yj;
             }
             if (tid < kb) y[k0 + tid] = yi;
+            if (K == 5) SOLVE_STAMP(17);
         } else {
             const double *row = Ad + (size_t)min(i1, n - 1) + (size_t)k0 * n;
 #pragma unroll
             for (int p = 0; p < kTile; ++p) cf[p] = row[(size_t)min(p, kb - 1) * n];
         }
         __syncthreads();
+        if (K == 5) SOLVE_STAMP(18);
         if (tid >= 64) {
-            if (i1 < fend && d.tile_first[i1 / kTile] <= K) {
+            if (i1 < fend && tile_first(i1 / kTile) <= K) {
                 double s = 0.0;
 #pragma unroll
                 for (int p = 0; p < kTile; ++p)
@@ -1012,16 +1030,18 @@ __device__ __forceinline__ void dense_solve_wg(const Dev &d) {
                 y[i1] -= s;
             }
             for (int i = i1 + kRowThreads; i < fend; i += kRowThreads) {  // n > ~kFacThreads only
-                if (d.tile_first[i / kTile] > K) continue;
+                if (tile_first(i / kTile) > K) continue;
                 double s = 0.0;
                 for (int p = 0; p < kb; ++p) s += Ad[(size_t)i + (size_t)(k0 + p) * n] * y[k0 + p];
                 y[i] -= s;
             }
         }
         __syncthreads();
+        if (K == 5) SOLVE_STAMP(19);
     }
     for (int i = tid; i < n; i += kFacThreads) y[i] = y[i] / Ad[(size_t)i + (size_t)i * n];
     __syncthreads();
+    SOLVE_STAMP(13);
     // backward: Lᵀ x = y, tile by tile from the bottom
     for (int K = nt - 1; K >= 0; --K) {
         const int k0 = K * kTile, kb = min(kTile, n - k0);
@@ -1030,13 +1050,27 @@ __device__ __forceinline__ void dense_solve_wg(const Dev &d) {
         // wave reads two columns, 32 consecutive rows each
         const int bend = min(n, (d.tile_last[K] + 1) * kTile);
         {
+            // one tile of rows per step (the stride is kTile rows): U tiles' loads in flight at
+            // once, clamped valid addresses, masked after; summed in row order
+            static_assert(kFacThreads / kTile == kTile, "one row of each tile per partial");
+            constexpr int U = 8;
             const int part = tid % kTile, c = tid / kTile;
             double s = 0.0;
             if (c < kb) {
-#pragma unroll 4
-                for (int i = k0 + kb + part; i < bend; i += kFacThreads / kTile) {
-                    if (d.tile_first[i / kTile] > K) continue;
-                    s += Ad[(size_t)i + (size_t)(k0 + c) * n] * y[i];
+                const double *colp = Ad + (size_t)(k0 + c) * n;
+                for (int m0 = K + 1; m0 * kTile < bend; m0 += U) {
+                    double v[U], yy[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int i = (m0 + u) * kTile + part;
+                        const bool ok = i < bend && tile_first(min(m0 + u, nt - 1)) <= K;
+                        const int ic = min(i, n - 1);
+                        v[u] = colp[ic];
+                        yy[u] = ok ? y[ic] : 0.0;
+                        v[u] = ok ? v[u] : 0.0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) s += v[u] * yy[u];
                 }
             }
             red[part][c] = s;

@@ -25,4 +25,8 @@ p = (st[:7] - st[0]) / 100.0
 u = (st[8:11] - st[8]) / 100.0
 print("panel  us (from after the guard): solve_ok read %.2f loads-issued %.2f diag-LDLT %.2f L-scale %.2f TRSM %.2f stores %.2f" % tuple(p[1:7]))
 print("update us: staged %.2f mfma %.2f" % tuple(u[1:3]))
+v = (st[12:16] - st[12]) / 100.0
+print("solve  us: forward %.2f backward %.2f pose-update %.2f" % (v[1], v[2] - v[1], v[3] - v[2]))
+w = (st[16:20] - st[16]) / 100.0
+print("forward tile K=5 us: wave0 chain done %.2f first barrier %.2f second barrier %.2f" % tuple(w[1:4]))
 s.close()
