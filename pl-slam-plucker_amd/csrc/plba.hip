@@ -908,7 +908,11 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_lms, d.n_lms_blocks);
     d.fold = sharded ? 0 : 1;
     d.fold_init = d.fold && !getenv("PLBA_NO_FOLD_INIT");
-    ZALLOC(d.cnt, 2 + (size_t)nblk + nf);  // arrival counters: lm_solve, iter_reduce, RCS blocks, poses
+    // arrival counters: lm_solve, iter_reduce (top), RCS blocks, poses, iter_reduce groups
+    const int nred = kPoseParts * nf + (d.n_lm > 0 ? d.n_lm_blocks : 0), ngrp = (nred + kRedGrp - 1) / kRedGrp;
+    ZALLOC(d.cnt, 2 + (size_t)nblk + nf + ngrp);
+    ALLOC(d.wg_red, 3 * (size_t)std::max(nred, 1));
+    ALLOC(d.grp_red, 3 * (size_t)std::max(ngrp, 1));
     d.n_ps = std::max(d.n_kf_blocks, d.bcr_N);
     ZALLOC(d.part_ps, d.n_ps);
     ZALLOC(d.ctrl, 1);

@@ -129,6 +129,7 @@ struct Dev {
     double *zb;                         // [nf][6]         z = D_B^{-1} y
     // reductions
     double *part_chi2;                  // [n_lin_blocks]
+    double *wg_red, *grp_red;           // folded init: [nred][3], [ceil(nred/64)][3] (χ², max, any)
     int32_t *part_any;                  // [n_lm_blocks] block has an active landmark
     double *part_max;                   // [nf + n_lm_blocks] (landmark part from nf on)
     double *part_lm, *part_lms;         // [n_lms_blocks] trial χ² partials, scale partials (k_lm_solve)
@@ -423,7 +424,8 @@ constexpr int kInitNT = 1024;  // k_iter_init / k_iter_pack: one wide workgroup 
 // packed lower-triangular index for 4x4 symmetric
 __device__ __forceinline__ constexpr int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
-__device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
+// returns max|Hpp_jj| of pose h in the workgroup that combined it (folded init), else 0
+__device__ __forceinline__ double pose_partial(const Dev &d, int h, int part) {
     double acc[kPP];
 #pragma unroll
     for (int k = 0; k < kPP; ++k) acc[k] = 0.0;
@@ -496,10 +498,13 @@ __device__ __forceinline__ void pose_partial(const Dev &d, int h, int part) {
         }
         const double m = wave_max(fabs(v));  // kLmBlock = one wave
         if (threadIdx.x == 0) st_sc1(d.part_max + h, m);
+        return m;
     }
+    return 0.0;
 }
 
-__device__ __forceinline__ void landmark_reduce(const Dev &d, int lb) {
+// returns (block max|H_ll diag|, block has an active landmark) through mx_out / any_out
+__device__ __forceinline__ void landmark_reduce(const Dev &d, int lb, double &mx_out, int &any_out) {
     __shared__ double sh[kLmBlock / 64];
     const int l = lb * kLmBlock + threadIdx.x;
     const bool sw = d.ctrl->switch_pending;
@@ -579,6 +584,8 @@ __device__ __forceinline__ void landmark_reduce(const Dev &d, int lb) {
         st_sc1(d.part_max + d.nf + lb, m);
         __hip_atomic_store(d.part_any + lb, anyb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    mx_out = m;
+    any_out = anyb;
 }
 
 
@@ -635,7 +642,8 @@ __global__ __launch_bounds__(kInitNT) void k_iter_pack(Dev d) {
 // the iteration init (k_iter_init's work): run as its own launch (sharded windows, windows with
 // nothing to reduce) or as the tail of the last-arriving k_iter_reduce workgroup (SC1: the
 // partials of that launch are read write-through)
-template <int NT, bool SC1>
+__device__ __forceinline__ void iter_init_ctrl(const Dev &d, double chi, double mx, bool any);
+template <int NT>
 __device__ __forceinline__ void iter_init_body(const Dev &d, double *sh) {
     double chi, mx;
     bool any;
@@ -647,40 +655,6 @@ __device__ __forceinline__ void iter_init_body(const Dev &d, double *sh) {
         mx = block_max<NT>(m, sh);
         chi = o[0];
         any = o[1] != 0.0;
-    } else if (SC1) {
-        // folded: the pose maxima are in part_max[0, nf) (per-pose combine), the landmark ones
-        // after them; every partial of this launch is read write-through, U loads in flight
-        constexpr int U = 8;
-        double s = 0.0, m = 0.0;
-        int a = 0;
-        for (int i0 = threadIdx.x; i0 < d.n_lin_blocks; i0 += NT * U) {
-            double v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = i0 + u * NT < d.n_lin_blocks ? d.part_chi2[i0 + u * NT] : 0.0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) s += v[u];
-        }
-        const int nm = d.nf + d.n_lm_blocks;
-        for (int i0 = threadIdx.x; i0 < nm; i0 += NT * U) {
-            double v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = i0 + u * NT < nm ? ld_sc1(d.part_max + i0 + u * NT) : 0.0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) m = fmax(m, v[u]);
-        }
-        for (int i0 = threadIdx.x; i0 < d.n_lm_blocks; i0 += NT * U) {
-            int v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                v[u] = i0 + u * NT < d.n_lm_blocks
-                           ? __hip_atomic_load(d.part_any + i0 + u * NT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : 0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) a |= v[u];
-        }
-        chi = block_sum<NT>(s, sh);
-        mx = block_max<NT>(m, sh);
-        any = __syncthreads_or(a) != 0;
     } else {
         double m = pose_combine<NT>(d, d.Hpp_w, d.bp_w);
         double s = 0.0;
@@ -692,7 +666,11 @@ __device__ __forceinline__ void iter_init_body(const Dev &d, double *sh) {
         for (int i = threadIdx.x; i < d.n_lm_blocks; i += NT) a |= d.part_any[i];
         any = __syncthreads_or(a) != 0;
     }
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) iter_init_ctrl(d, chi, mx, any);
+}
+// the control part of the iteration init (one thread): stage switch, λ init / hand-rolled stops
+__device__ __forceinline__ void iter_init_ctrl(const Dev &d, double chi, double mx, bool any) {
+    {
         Ctrl *c = d.ctrl;
         if (c->switch_pending) {  // initializeOptimization(level) of the next stage
             c->switch_pending = 0;
@@ -750,18 +728,85 @@ __device__ __forceinline__ void iter_init_body(const Dev &d, double *sh) {
 __global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
     ITER_GUARD
     __shared__ double sh[kInitNT / 64];
-    iter_init_body<kInitNT, false>(d, sh);
+    iter_init_body<kInitNT>(d, sh);
 }
 
+constexpr int kRedGrp = 256;  // k_iter_reduce workgroups per first-level group of the folded init
 __global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
     ITER_GUARD
     __shared__ double sh_init[kLmBlock / 64];
     const int b = blockIdx.x, np = kPoseParts * d.nf;
-    if (b < np) pose_partial(d, b / kPoseParts, b % kPoseParts);  // workgroup-uniform branch
-    else landmark_reduce(d, b - np);
-    // the last workgroup to finish runs the iteration init (k_iter_init's work; the pose
-    // combine already ran per pose)
-    if (d.fold_init && arrive_last(d.cnt + 1, (int32_t)gridDim.x)) iter_init_body<kLmBlock, true>(d, sh_init);
+    const int G = (int)gridDim.x, lane = threadIdx.x;
+    // folded init: this workgroup's slice of k_linearize's χ² partials, loaded before the main
+    // work so the round trip overlaps it
+    double sc = 0.0;
+    if (d.fold_init) {
+        const int lo = (int)((long long)b * d.n_lin_blocks / G), hi = (int)((long long)(b + 1) * d.n_lin_blocks / G);
+        for (int i = lo + lane; i < hi; i += kLmBlock) sc += d.part_chi2[i];
+    }
+    double wmax = 0.0;
+    int wany = 0;
+    if (b < np) wmax = pose_partial(d, b / kPoseParts, b % kPoseParts);  // workgroup-uniform branch
+    else landmark_reduce(d, b - np, wmax, wany);
+    if (!d.fold_init) return;
+    // folded iteration init (k_iter_init's work; the pose combine already ran per pose), reduced
+    // in two levels so no single workgroup reads every partial: each workgroup adds a slice of
+    // k_linearize's χ² partials to its own (max, any), the last of each group of kRedGrp
+    // workgroups combines the group, the last group runs the control step. Fixed order.
+    {
+        sc = wave_sum(sc);  // kLmBlock = one wave
+        if (lane == 0) {
+            st_sc1(d.wg_red + 3 * (size_t)b, sc);
+            st_sc1(d.wg_red + 3 * (size_t)b + 1, wmax);
+            st_sc1(d.wg_red + 3 * (size_t)b + 2, wany ? 1.0 : 0.0);
+        }
+    }
+    constexpr int U = kRedGrp / kLmBlock;
+    const int g = b / kRedGrp, gn = min(kRedGrp, G - kRedGrp * g), ng = (G + kRedGrp - 1) / kRedGrp;
+    if (!arrive_last(d.cnt + 2 + d.nblk + d.nf + g, gn)) return;
+    {
+        double cv[U], mv[U], av[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // lane holds members lane·U .. lane·U+U-1, all loads in flight
+            const int k = lane * U + u;
+            const double *w = d.wg_red + 3 * (size_t)(kRedGrp * g + min(k, gn - 1));
+            cv[u] = ld_sc1(w);
+            mv[u] = ld_sc1(w + 1);
+            av[u] = ld_sc1(w + 2);
+        }
+        double c = 0.0, m = 0.0, a = 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (lane * U + u < gn) {
+                c += cv[u];
+                m = fmax(m, mv[u]);
+                a = fmax(a, av[u]);
+            }
+        c = wave_sum(c);
+        m = wave_max(m);
+        a = wave_max(a);
+        if (lane == 0) {
+            st_sc1(d.grp_red + 3 * (size_t)g, c);
+            st_sc1(d.grp_red + 3 * (size_t)g + 1, m);
+            st_sc1(d.grp_red + 3 * (size_t)g + 2, a);
+        }
+    }
+    if (!arrive_last(d.cnt + 1, ng)) return;
+    double c = 0.0, m = 0.0, a = 0.0;
+    for (int g0 = 0; g0 < ng; g0 += 64) {  // groups in index order, 64 at a time
+        double cg = 0.0, mg = 0.0, ag = 0.0;
+        if (g0 + lane < ng) {
+            const double *w = d.grp_red + 3 * (size_t)(g0 + lane);
+            cg = ld_sc1(w);
+            mg = ld_sc1(w + 1);
+            ag = ld_sc1(w + 2);
+        }
+        c += wave_sum(cg);
+        m = fmax(m, wave_max(mg));
+        a = fmax(a, wave_max(ag));
+    }
+    (void)sh_init;
+    if (lane == 0) iter_init_ctrl(d, c, m, a != 0.0);
 }
 
 // ---------------------------------------------------------------- reduced camera system
