@@ -94,7 +94,26 @@ def cpu_baseline(cfg: str, runs: int):
         os.sched_setaffinity(0, prev)
     med = statistics.median(ms)
     it = iters[0]
-    return dict(value=it / (med / 1e3), unit="LM iterations/s", cores=1, kind="port",
+    # refcpu-fast: the same restatement with fixed-size blocks — a sanity lower
+    # bound reported beside the baseline, not the speedup basis
+    fast = None
+    try:
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-s", "fast"], check=True)
+        oa._lib = None
+        oa.ORACLE_SO = os.path.join(ROOT, "oracle", "librefcpu_fast_native.so")
+        os.sched_setaffinity(0, {core})
+        try:
+            oa.lba_plucker(g)
+            fms = [oa.lba_plucker(g)["solve_ms"] for _ in range(runs)]
+        finally:
+            os.sched_setaffinity(0, prev)
+        fmed = statistics.median(fms)
+        fast = dict(value=it / (fmed / 1e3), ms_per_lba=fmed, kind="port-fast",
+                    note="oracle/refcpu.cpp -DREFCPU_FAST: inline fixed-capacity blocks, compile-time "
+                         "Schur / quadratic-form block sizes, pair->block lookups resolved once; same results")
+    except Exception as e:  # the lower bound is informational
+        fast = {"error": repr(e)}
+    return dict(value=it / (med / 1e3), unit="LM iterations/s", cores=1, kind="port", refcpu_fast=fast,
                 cpu_model=cpu_model(), pinned_core=core, host_cpus=os.cpu_count(),
                 final_chi2=[float(r["chi2"][0]), float(r["chi2"][1])],
                 sample=f"{cfg} window ({g.n_kf} KF, {g.n_pt} pts, {g.n_ln} lines, {g.n_ept + g.n_eln} edges), "

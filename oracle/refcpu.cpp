@@ -314,6 +314,7 @@ inline void huber(double e, double delta, double rho[3]) {
 // ------------------------------------------------------------------------------------
 // dynamic-size dense block (Eigen::MatrixXd-like, column-major, heap storage)
 // ------------------------------------------------------------------------------------
+#ifndef REFCPU_FAST
 struct DMat {
     int r = 0, c = 0;
     std::vector<double> a;
@@ -323,6 +324,19 @@ struct DMat {
     double operator()(int i, int j) const { return a[(size_t)i + (size_t)j * r]; }
     void setZero() { std::fill(a.begin(), a.end(), 0.0); }
 };
+#else
+// refcpu-fast (BASELINE.md §2 lower bound): the same blocks with inline fixed-capacity storage
+// (every block of this path is at most 6x6) — no heap traffic per block or temporary
+struct DMat {
+    int r = 0, c = 0;
+    double a[36];
+    DMat() {}
+    DMat(int r_, int c_) : r(r_), c(c_) { setZero(); }
+    double &operator()(int i, int j) { return a[i + j * r]; }
+    double operator()(int i, int j) const { return a[i + j * r]; }
+    void setZero() { for (int k = 0; k < r * c; ++k) a[k] = 0.0; }
+};
+#endif
 inline DMat mul(const DMat &A, const DMat &B) {  // heap temporary, like an Eigen dynamic product
     DMat C(A.r, B.c);
     for (int j = 0; j < B.c; ++j)
@@ -364,7 +378,11 @@ inline DMat lu_inverse(const DMat &D) {
     }
     DMat X(n, n);
     for (int col = 0; col < n; ++col) {
+#ifdef REFCPU_FAST
+        double y[6];
+#else
         std::vector<double> y(n);
+#endif
         for (int i = 0; i < n; ++i) y[i] = (perm[i] == col) ? 1.0 : 0.0;
         for (int i = 0; i < n; ++i)
             for (int k = 0; k < i; ++k) y[i] -= LU(i, k) * y[k];
@@ -444,8 +462,16 @@ struct Edge {
     bool allVerticesFixed() const { return v[0]->fixed && v[1]->fixed; }
     // BaseBinaryEdge::constructQuadraticForm (g2o core), Ω = info·I
     void constructQuadraticForm() {
+#ifdef REFCPU_FAST  // fixed-size blocks: point (3, D 2) and line (4, D 4) edges compiled per shape
+        if (v[0]->dim == 3 && D == 2) return quadratic_form<3, 2>();
+        if (v[0]->dim == 4 && D == 4) return quadratic_form<4, 4>();
+#endif
+        quadratic_form<0, 0>();
+    }
+    template <int DI, int DD>  // 0: runtime size
+    void quadratic_form() {
         Vertex *from = v[0], *to = v[1];
-        const int di = from->dim, dj = 6;
+        const int di = DI > 0 ? DI : from->dim, dj = 6, D = DD > 0 ? DD : this->D;
         bool fromNotFixed = !from->fixed, toNotFixed = !to->fixed;
         if (!(fromNotFixed || toNotFixed)) return;
         double omega_r[4];
@@ -670,6 +696,9 @@ struct BlockSolverX {
     // Hschur upper structure: column i2 -> sorted (row i1 <= i2, block); and row-major lookup
     std::vector<std::vector<std::pair<int, DMat *>>> schurCols;
     std::vector<std::map<int, DMat *>> schurRow;  // row i1 -> (col i2 >= i1, block)
+#ifdef REFCPU_FAST
+    std::vector<std::vector<DMat *>> pairBlk;      // per landmark: Hschur block of each (a <= c2) pair
+#endif
     std::vector<double> x, b, coeff, bschur;
     std::vector<std::vector<double>> diagBackupP, diagBackupL;
     std::vector<DMat> Dinv;
@@ -716,6 +745,14 @@ struct BlockSolverX {
         for (int i1 = 0; i1 < numPoses; ++i1)
             for (auto &kv : schurRow[i1]) schurCols[kv.first].push_back({i1, kv.second});
         for (auto &c : schurCols) std::sort(c.begin(), c.end(), [](auto &a, auto &b) { return a.first < b.first; });
+#ifdef REFCPU_FAST
+        pairBlk.assign(numLandmarks, {});
+        for (int l = 0; l < numLandmarks; ++l) {
+            const auto &colL = HplCCS[l];
+            for (size_t a = 0; a < colL.size(); ++a)
+                for (size_t c2 = a; c2 < colL.size(); ++c2) pairBlk[l].push_back(schurRow[colL[a].first].at(colL[c2].first));
+        }
+#endif
         x.assign(sizePoses + sizeLandmarks, 0.0);
         b.assign(sizePoses + sizeLandmarks, 0.0);
         coeff.assign(sizePoses + sizeLandmarks, 0.0);
@@ -758,6 +795,49 @@ struct BlockSolverX {
             for (int k = 0; k < HllDiag[i]->r; ++k) (*HllDiag[i])(k, k) = diagBackupL[i][k];
     }
 
+#ifdef REFCPU_FAST
+    // refcpu-fast: one landmark's Schur contribution with compile-time block sizes (same
+    // products in the same summation order as the heap-block path below)
+    template <int DL>
+    void schur_landmark(int l, int base) {
+        const DMat &D = *HllDiag[l];
+        Dinv[l] = lu_inverse(D);
+        const DMat &Di = Dinv[l];
+        double db[DL];
+        for (int i = 0; i < DL; ++i) {
+            double acc = 0.0;
+            for (int k = 0; k < DL; ++k) acc += Di(i, k) * b[sizePoses + base + k];
+            db[i] = acc;
+        }
+        auto &colL = HplCCS[l];
+        DMat *const *pb = pairBlk[l].data();
+        for (size_t a = 0; a < colL.size(); ++a) {
+            const int i1 = colL[a].first;
+            const double *Bi = colL[a].second->a;  // 6 x DL column-major
+            double BD[6 * DL];                     // Bi·Dinv, column-major
+            for (int j = 0; j < DL; ++j)
+                for (int i = 0; i < 6; ++i) BD[i + 6 * j] = 0.0;
+            for (int j = 0; j < DL; ++j)
+                for (int k = 0; k < DL; ++k) {
+                    const double dkj = Di(k, j);
+                    for (int i = 0; i < 6; ++i) BD[i + 6 * j] += Bi[i + 6 * k] * dkj;
+                }
+            double Bb[6] = {0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < DL; ++k)
+                for (int i = 0; i < 6; ++i) Bb[i] += Bi[i + 6 * k] * db[k];
+            for (int k = 0; k < 6; ++k) coeff[i1 * 6 + k] += Bb[k];
+            for (size_t c2 = a; c2 < colL.size(); ++c2) {
+                double *C = (*pb++)->a;
+                const double *B2 = colL[c2].second->a;
+                for (int j = 0; j < 6; ++j)
+                    for (int k = 0; k < DL; ++k) {
+                        const double bjk = B2[j + 6 * k];
+                        for (int i = 0; i < 6; ++i) C[i + 6 * j] -= BD[i + 6 * k] * bjk;
+                    }
+            }
+        }
+    }
+#endif
     bool solve() {
         // _Hschur = _Hpp (keeping the pattern of _Hschur)
         for (int i = 0; i < numPoses; ++i)
@@ -773,22 +853,33 @@ struct BlockSolverX {
         }
         for (int l = 0; l < numLandmarks; ++l) {
             const DMat &D = *HllDiag[l];
+#ifdef REFCPU_FAST
+            if (D.r == 3) { schur_landmark<3>(l, lmBase[l]); continue; }
+            if (D.r == 4) { schur_landmark<4>(l, lmBase[l]); continue; }
+#endif
             Dinv[l] = lu_inverse(D);
             DMat db(D.r, 1);
             for (int j = 0; j < D.r; ++j) db(j, 0) = b[sizePoses + lmBase[l] + j];
             db = mul(Dinv[l], db);
             auto &colL = HplCCS[l];
+#ifdef REFCPU_FAST
+            DMat *const *pb = pairBlk[l].data();
+#endif
             for (size_t a = 0; a < colL.size(); ++a) {
                 int i1 = colL[a].first;
                 const DMat &Bi = *colL[a].second;
                 DMat BDinv = mul(Bi, Dinv[l]);
                 DMat Bb = mul(Bi, db);
                 for (int k = 0; k < 6; ++k) coeff[i1 * 6 + k] += Bb(k, 0);
+#ifdef REFCPU_FAST
+                for (size_t c2 = a; c2 < colL.size(); ++c2) sub_mul_transB(**pb++, BDinv, *colL[c2].second);
+#else
                 auto &row = schurRow[i1];
                 for (size_t c2 = a; c2 < colL.size(); ++c2) {
                     int i2 = colL[c2].first;
                     sub_mul_transB(*row.at(i2), BDinv, *colL[c2].second);
                 }
+#endif
             }
         }
         for (int i = 0; i < sizePoses; ++i) bschur[i] = b[i] - coeff[i];
