@@ -470,7 +470,9 @@ __device__ __forceinline__ double pose_partial(const Dev &d, int h, int part) {
     }
     // folded iteration init: the last of the pose's kPoseParts workgroups adds the parts (in part
     // order, as pose_combine does) into Hpp / b_p / active count and publishes max|Hpp_jj|
-    if (d.fold_init && arrive_last(d.cnt + 2 + d.nblk + h, kPoseParts)) {
+    // (sharded windows too: the combine then writes this rank's partial Hpp / b_p into the
+    // all-reduce source, and k_iter_pack only packs χ² and the landmark maxima)
+    if ((d.fold_init || d.sharded) && arrive_last(d.cnt + 2 + d.nblk + h, kPoseParts)) {
         const int k = threadIdx.x;
         double v = 0.0;
         if (k < kPP) {
@@ -621,7 +623,7 @@ __device__ __forceinline__ double pose_combine(const Dev &d, double *H, double *
 __global__ __launch_bounds__(kInitNT) void k_iter_pack(Dev d) {
     ITER_GUARD
     __shared__ double sh[kInitNT / 64];
-    (void)pose_combine<kInitNT>(d, d.Hpp_w, d.bp_w);
+    // (Hpp / b_p / active counts: combined per pose by the last of its k_iter_reduce parts)
     double s = 0.0;
     for (int i = threadIdx.x; i < d.n_lin_blocks; i += kInitNT) s += d.part_chi2[i];
     const double chi = block_sum<kInitNT>(s, sh);
