@@ -315,6 +315,12 @@ const void *bcr_kernel_impl(int bw, std::integer_sequence<int, B...>) {
 }
 inline const void *bcr_kernel(int bw) { return bcr_kernel_impl(bw, std::make_integer_sequence<int, kBcrMaxBW + 1>{}); }
 inline size_t bcr_lds_bytes(int bw) { return sizeof(double) * bcr_lds_doubles(bw); }
+// n up to which the dense solve keeps y in LDS; PLBA_SOLVE_LDS_N lowers it (tests: the global-y path
+// at sizes the oracle finishes)
+inline int solve_lds_limit() {
+    const char *e = getenv("PLBA_SOLVE_LDS_N");
+    return e && e[0] ? std::min(atoi(e), kSolveLdsN) : kSolveLdsN;
+}
 // Factorisation mode of a banded window: PLBA_FACTOR=bcr|cl|band forces one (diagnostics / A-B
 // runs); by default block cyclic reduction once the window has enough super-rows for its
 // log-depth chain to beat the two-sided column-lane chain of (nf+bw)/2 pivot steps.
@@ -793,6 +799,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         const char *dg = getenv("PLBA_DIAG");
         d.diag = dg ? atoi(dg) : 0;
     }
+    d.solve_lds_n = solve_lds_limit();
     d.cam = Cam{g->fx, g->fy, g->cx, g->cy};
     d.huber_pt = g->huber_pt;
     d.huber_ln = g->huber_ln;
@@ -1030,7 +1037,7 @@ int launch_step(plba_ctx *ctx) {
         }
         if (!(d.fold && d.nch > 0))  // (folded into the last chunk of each block otherwise)
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
-        const size_t solve_lds = d.n <= kSolveLdsN ? sizeof(double) * (size_t)d.n : 0;  // y of dense_solve_wg
+        const size_t solve_lds = d.n <= d.solve_lds_n ? sizeof(double) * (size_t)d.n : 0;  // y of dense_solve_wg
         if (d.band_mode) {
             LAUNCH(K_FACTOR, launch_band(d, s));
         } else if (d.dense_mfma) {  // blocked LDLᵀ, MFMA trailing updates (plba_dense.hpp)
@@ -1987,6 +1994,7 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
     P.T[0] = T0; P.T[1] = T1;
     P.blk_r = blk_r_d; P.blk_c = blk_c_d; P.blk_off = blk_off_d; P.blk_con = blk_con_d;
     dd.n = n; dd.ntiles = ntiles; dd.Ad = Ad; dd.bs = P.b; dd.xp = P.x; dd.ctrl = ctrl_d;
+    dd.solve_lds_n = solve_lds_limit();
     dd.tile_first = tf_d; dd.tile_last = tl_d;
     double *hout = ctx->pgo_hout;
     auto fetch = [&]() -> int {
@@ -2034,7 +2042,7 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
             }
             hipLaunchKernelGGL(k_pgo_check, dim3(1), dim3(256), 0, s, dd);
             hipLaunchKernelGGL(k_pgo_solve, dim3(1), dim3(kFacThreads),
-                               n <= kSolveLdsN ? sizeof(double) * (size_t)n : 0, s, dd);
+                               n <= dd.solve_lds_n ? sizeof(double) * (size_t)n : 0, s, dd);
             hipLaunchKernelGGL(k_pgo_update, dim3((nv + kPgoNT - 1) / kPgoNT), dim3(kPgoNT), 0, s, P, cur);
             // restoreDiagonal (Hd is untouched), computeActiveErrors at the trial state
             hipLaunchKernelGGL(k_pgo_linearize<false>, dim3(eb), dim3(kPgoNT), 0, s, P, cur ^ 1);

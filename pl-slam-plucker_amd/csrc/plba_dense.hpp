@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kFacThreads) void k_dense_solve(Dev d) {
     TRIAL_GUARD
     SOLVE_STAMP(12);
     if (d.ctrl->solve_ok) {  // forward substitution done by the panels / updates (dense_yd)
-        if (d.n <= kSolveLdsN) dense_solve_wg<true, true>(d);
+        if (d.n <= d.solve_lds_n) dense_solve_wg<true, true>(d);
         else dense_solve_wg<false, true>(d);
     }
     __syncthreads();

@@ -78,6 +78,7 @@ struct Ctrl {
 struct Dev {
     int32_t n_kf, n_pt, n_ln, n_lm, Ep, El, E, nf, n;
     int32_t corrected, n_lin_blocks, n_lm_blocks, n_kf_blocks, nblk, ntiles;
+    int32_t solve_lds_n;                // dense solve: y in LDS up to this n (kSolveLdsN; tests lower it)
     int32_t n_lms_blocks;               // k_lm_solve workgroups (kLmLanes lanes per landmark)
     Cam cam;
     double huber_pt, huber_ln, tau;
@@ -1237,7 +1238,7 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
     __syncthreads();
     if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
     if (!s_fail) {  // on failure x_p keeps its previous value (g2o leaves _x untouched)
-        if (n <= kSolveLdsN) dense_solve_wg<true>(d);
+        if (n <= d.solve_lds_n) dense_solve_wg<true>(d);
         else dense_solve_wg<false>(d);
     }
     __syncthreads();

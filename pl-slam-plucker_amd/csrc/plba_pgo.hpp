@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) void k_pgo_check(Dev d) {
 
 __global__ __launch_bounds__(kFacThreads) void k_pgo_solve(Dev d) {
     if (!d.ctrl->solve_ok) return;  // x keeps its previous value (g2o's _x)
-    if (d.n <= kSolveLdsN) dense_solve_wg<true, true>(d);  // forward part done in the factorisation
+    if (d.n <= d.solve_lds_n) dense_solve_wg<true, true>(d);  // forward part done in the factorisation
     else dense_solve_wg<false, true>(d);
 }
 

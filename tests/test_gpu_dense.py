@@ -103,3 +103,21 @@ def test_dense_mfma_hand_rolled_lm(solver, monkeypatch):
     assert out["linearizations"] == ref["linearizations"] and out["accepted"] == ref["accepted"]
     d = np.abs(ref["pt_xyz"] - win.graph.pt_xyz).max()
     assert np.abs(out["pt_xyz"] - ref["pt_xyz"]).max() <= 1e-4 * d + 1e-12
+
+
+def test_dense_solve_with_y_in_global_memory(solver, monkeypatch):
+    """Windows with n > kSolveLdsN keep the substitution vector in global memory instead of LDS;
+    PLBA_SOLVE_LDS_N=0 takes that path at a size the oracle finishes. Same operations in the same
+    order as the LDS path, so the two agree bitwise."""
+    monkeypatch.setenv("PLBA_NO_RCM", "1")
+    g = synth.generate("C1", n_kf=30, n_pt=400, seed=35, track_max=30)
+    ref = oa.lba_plucker(g)
+    solver.upload(g)
+    assert solver.structure_stats()["dense_mfma"] == 1
+    lds = solver.lba_plucker()
+    monkeypatch.setenv("PLBA_SOLVE_LDS_N", "0")
+    solver.upload(g)
+    glob = solver.lba_plucker()
+    _check(glob, ref)
+    np.testing.assert_array_equal(glob["kf_Tcw"], lds["kf_Tcw"])
+    np.testing.assert_array_equal(glob["pt_xyz"], lds["pt_xyz"])

@@ -93,3 +93,15 @@ def test_pgo_leaves_an_uploaded_window_intact(solver):
     solver.reset()
     after = solver.lba_plucker()
     assert np.array_equal(before["kf_Tcw"], after["kf_Tcw"])
+
+
+def test_pgo_solve_with_y_in_global_memory(solver, monkeypatch):
+    """Pose graphs with n > kSolveLdsN (about 1000 keyframes) substitute with y in global memory;
+    PLBA_SOLVE_LDS_N=0 takes that path on a graph the oracle finishes: same as the LDS path
+    bitwise, and the oracle's trajectory."""
+    pg = pgo.loop_graph(n_kf=60, seed=5, cov_window=5, extra_loops=3)
+    lds = solver.pgo_optimize(pg)
+    monkeypatch.setenv("PLBA_SOLVE_LDS_N", "0")
+    out = solver.pgo_optimize(pg)
+    np.testing.assert_array_equal(out["v_T"], lds["v_T"])
+    _compare(out, oa.pgo_optimize(pg))
