@@ -1013,6 +1013,8 @@ int allreduce(plba_ctx *ctx, const double *send, double *recv, size_t n) {
 int launch_step(plba_ctx *ctx) {
     Dev &d = ctx->d;
     hipStream_t s = ctx->stream;
+    // PLBA_CHUNK_DIRECT=1: per-lane A/Z row loads in the Schur assembly (A/B of the staged copy)
+    static const bool chunk_direct = getenv("PLBA_CHUNK_DIRECT") != nullptr;
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     if (d.nf > 0 || d.n_lm > 0) {
         const int nred = kPoseParts * d.nf + (d.n_lm > 0 ? d.n_lm_blocks : 0);
@@ -1030,7 +1032,7 @@ int launch_step(plba_ctx *ctx) {
     }
     if (d.n > 0) {
         if (!d.band_mode) LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
-        if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(k_rcs_chunk, dim3(d.nch), dim3(64), 0, s, d));
+        if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(chunk_direct ? k_rcs_chunk<false> : k_rcs_chunk<true>, dim3(d.nch), dim3(64), 0, s, d));
         if (d.sharded) {
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
             COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);

@@ -851,9 +851,17 @@ __device__ __forceinline__ void rcs_finalize_entry(const Dev &d, int b, int e, d
 // Chunked reduced-camera assembly, pass 1: one wave per chunk of <= kChunk triples of one
 // block; each lane accumulates A₁ᵀ(Z₁Z₂ᵀ)A₂ (36) and, for self-triples of a diagonal block,
 // A_eᵀ q_e (6); the wave reduces through LDS in fixed lane order (deterministic).
+// STAGED (default): the 64 triples of a batch fetch their A/Z rows cooperatively — load j of
+// the wave covers rows (64j + lane)/6 of the batch's A₁ (16 B per lane, consecutive lanes on
+// consecutive pieces of one 96-B row), so one load instruction touches ~8-16 cache lines
+// instead of 64 (one per lane and piece); the rows land in LDS and every lane then reads its
+// own row. The arithmetic per lane is unchanged (bitwise-identical sums).
+typedef double dbl2 __attribute__((ext_vector_type(2)));  // register-promotable 16-B pair
+template <bool STAGED>
 __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
     TRIAL_GUARD
-    __shared__ double red[64][43];
+    __shared__ double smem[64 * 43];  // staging: A₁ | A₂ (64x12) | Z₁ | Z₂ (64x8); then red[64][43]
+    double(*red)[43] = reinterpret_cast<double(*)[43]>(smem);
     // XCD-aware remap (blocks are dealt round-robin over the 8 XCDs): each XCD gets a contiguous
     // run of chunks = a contiguous range of RCS block rows, so the A/Z rows of the landmarks
     // they couple are re-read from that XCD's L2 instead of the fabric (speed only)
@@ -868,18 +876,57 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
 #pragma unroll
     for (int k = 0; k < 42; ++k) acc[k] = 0.0;
     const int t0 = d.ch_off[ch], t1 = d.ch_off[ch + 1];
-#pragma unroll
+#pragma unroll 1
     for (int q = 0; q < kChunk / 64; ++q) {
-        const int t = t0 + lane + 64 * q;
-        if (t < t1) {
-            const int e1 = d.trip[2 * t], e2 = d.trip[2 * t + 1];
+        const int tb = t0 + 64 * q;
+        if (tb >= t1) break;  // wave-uniform
+        const int t = tb + lane;
+        const int tt = t < t1 ? t : tb;  // rows past the chunk fetch a valid edge, add nothing
+        const int e1 = d.trip[2 * tt], e2 = d.trip[2 * tt + 1];
+        double z1[8], z2[8], a1[12], a2[12];
+        if (STAGED) {
+            dbl2 *sA1 = reinterpret_cast<dbl2 *>(smem), *sA2 = sA1 + 384;
+            dbl2 *sZ1 = sA2 + 384, *sZ2 = sZ1 + 256;
+            dbl2 v1[6], v2[6], w1[4], w2[4];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int pc = 64 * j + lane, r = pc / 6, k = pc - 6 * r;
+                const int f1 = __shfl(e1, r, 64), f2 = __shfl(e2, r, 64);
+                v1[j] = reinterpret_cast<const dbl2 *>(d.A + (size_t)f1 * 12)[k];
+                v2[j] = reinterpret_cast<const dbl2 *>(d.A + (size_t)f2 * 12)[k];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = 16 * j + (lane >> 2), k = lane & 3;
+                const int f1 = __shfl(e1, r, 64), f2 = __shfl(e2, r, 64);
+                w1[j] = reinterpret_cast<const dbl2 *>(d.Z + (size_t)f1 * 8)[k];
+                w2[j] = reinterpret_cast<const dbl2 *>(d.Z + (size_t)f2 * 8)[k];
+            }
+            __syncthreads();  // the previous batch's rows are read (one wave: a cheap barrier)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) { sA1[64 * j + lane] = v1[j]; sA2[64 * j + lane] = v2[j]; }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { sZ1[64 * j + lane] = w1[j]; sZ2[64 * j + lane] = w2[j]; }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const dbl2 x = sA1[6 * lane + k], y = sA2[6 * lane + k];
+                a1[2 * k] = x.x; a1[2 * k + 1] = x.y; a2[2 * k] = y.x; a2[2 * k + 1] = y.y;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const dbl2 x = sZ1[4 * lane + k], y = sZ2[4 * lane + k];
+                z1[2 * k] = x.x; z1[2 * k + 1] = x.y; z2[2 * k] = y.x; z2[2 * k + 1] = y.y;
+            }
+        } else {
             const double *Z1 = d.Z + (size_t)e1 * 8, *Z2 = d.Z + (size_t)e2 * 8;
             const double *A1 = d.A + (size_t)e1 * 12, *A2 = d.A + (size_t)e2 * 12;
-            double z1[8], z2[8], a1[12], a2[12];
 #pragma unroll
             for (int k = 0; k < 8; ++k) { z1[k] = Z1[k]; z2[k] = Z2[k]; }
 #pragma unroll
             for (int k = 0; k < 12; ++k) { a1[k] = A1[k]; a2[k] = A2[k]; }
+        }
+        if (t < t1) {
             double m00 = 0, m01 = 0, m10 = 0, m11 = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -908,6 +955,7 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
             }
         }
     }
+    if (STAGED) __syncthreads();  // the staging rows are read before red overwrites them
 #pragma unroll
     for (int k = 0; k < 42; ++k) red[lane][k] = acc[k];
     __syncthreads();
