@@ -55,11 +55,14 @@ __host__ __device__ constexpr size_t bcr_pub_doubles(int bw) { return (size_t)36
 // solution record of a super-row: x (6 bw) + failure word (propagated down the back substitution)
 __host__ __device__ constexpr int bcr_xrec(int bw) { return 6 * bw + 2; }
 
-// one lane: relaxed poll until the flag carries `epoch`; bounded (~0.3 s), timeout -> *err = 1
-__device__ __forceinline__ bool bcr_poll(uint32_t *flag, uint32_t epoch, int32_t *err) {
+// one lane: relaxed poll until the flag carries `epoch`; bounded (~0.3 s), timeout -> *err = 1.
+// PLBA_DIAG bit 64 (failure-path test only): the flag is checked once, so every hand-off that
+// is not already published times out and the solve must come back as PLBA_E_DEVICE
+__device__ __forceinline__ bool bcr_poll(uint32_t *flag, uint32_t epoch, int32_t *err, int diag) {
+    const uint32_t lim = (diag & 64) ? 0u : (1u << 23);
     for (uint32_t spins = 0;; ++spins) {
         if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return true;
-        if (spins >= (1u << 23)) {
+        if (spins >= lim) {
             __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
@@ -256,8 +259,8 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
         for (int lp = 0; lp < lm; ++lp) {
             const int na = m - (1 << lp), nb = m + (1 << lp);  // above (m is its c) / below (m is its a)
             const bool ha = na >= 0, hb = nb < N;
-            if (tid == 0 && ha && !bcr_poll(&d.bcr_flag[2 * na], s_epoch, &d.ctrl->dev_error)) s_fail = 1;
-            if (tid == 64 && hb && !bcr_poll(&d.bcr_flag[2 * nb], s_epoch, &d.ctrl->dev_error)) s_fail = 1;
+            if (tid == 0 && ha && !bcr_poll(&d.bcr_flag[2 * na], s_epoch, &d.ctrl->dev_error, d.diag)) s_fail = 1;
+            if (tid == 64 && hb && !bcr_poll(&d.bcr_flag[2 * nb], s_epoch, &d.ctrl->dev_error, d.diag)) s_fail = 1;
             __syncthreads();
             const double *pa = d.bcr_pub + (size_t)(ha ? na : 0) * PUB, *pb = d.bcr_pub + (size_t)(hb ? nb : 0) * PUB;
             const bool takeF = lm == lp + 1;  // the coupling created at level lm-1: U from above, V from below
@@ -458,8 +461,8 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
         double *xa = xv, *xc = xv + S, *xm = xv + 2 * S;
         double fail_tot = fail_fwd;  // root: everything has flowed in; others: from a (and c)
         if (!root) {
-            if (tid == 0 && !bcr_poll(&d.bcr_flag[2 * a_row + 1], epoch, &d.ctrl->dev_error)) s_fail = 1;
-            if (hasC && tid == 64 && !bcr_poll(&d.bcr_flag[2 * c_row + 1], epoch, &d.ctrl->dev_error)) s_fail = 1;
+            if (tid == 0 && !bcr_poll(&d.bcr_flag[2 * a_row + 1], epoch, &d.ctrl->dev_error, d.diag)) s_fail = 1;
+            if (hasC && tid == 64 && !bcr_poll(&d.bcr_flag[2 * c_row + 1], epoch, &d.ctrl->dev_error, d.diag)) s_fail = 1;
             __syncthreads();
             for (int t = tid; t < S; t += NT) {
                 xa[t] = ld_sc1(d.bcr_x + (size_t)a_row * XR + t);

@@ -325,3 +325,31 @@ def test_block_cyclic_reduction_matches_oracle(solver, monkeypatch, tmax, n_kf):
     cl = solver.lba_plucker()
     monkeypatch.delenv("PLBA_FACTOR")
     assert np.abs(out["kf_Tcw"] - cl["kf_Tcw"]).max() < 1e-9
+
+
+def test_bcr_handoff_timeout_reports_device_error(monkeypatch):
+    """The failure path of BCR's bounded hand-off waits (plba_bcr.hpp bcr_poll): with PLBA_DIAG
+    bit 64 every flag is checked once, so the waits of level >= 1 time out; the solve must come
+    back as PLBA_E_DEVICE (never a silently accepted step), and a fresh context afterwards solves
+    the same window normally."""
+    from plba.lib import Solver
+    g = synth.generate("C1L", n_kf=64, n_pt=1600, n_ln=320, seed=640, track_min=2, track_max=8,
+                       fixed_frac=0.1)
+    monkeypatch.setenv("PLBA_FACTOR", "bcr")
+    monkeypatch.setenv("PLBA_DIAG", "64")
+    s = Solver()
+    try:
+        s.upload(g)
+        assert s.structure_stats()["bcr_rows"] >= 4
+        with pytest.raises(Exception, match="PLBA_E_DEVICE|hand-off"):
+            s.lba_plucker()
+    finally:
+        s.close()
+    monkeypatch.delenv("PLBA_DIAG")
+    s = Solver()
+    try:
+        s.upload(g)
+        out = s.lba_plucker()
+    finally:
+        s.close()
+    _check(out, oa.lba_plucker(g))
