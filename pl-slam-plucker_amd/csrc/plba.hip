@@ -903,7 +903,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     }
     if (!band_mode) ZALLOC(d.bcr_stamps, kBcrStamps);  // dense-path phase stamps (PLBA_DIAG bit 8)
     ALLOC(d.bs, n);
-    ZALLOC(d.xp, n);
+    ZALLOC(d.xp, std::max(n, 6));  // k_lm_solve reads x_p[6·max(h, 0) ..] for fixed-pose slots too
     ALLOC(d.Wbuf, (size_t)std::max(n, 1) * (kTile + 1));  // W panel + y of the dense path
     UPLOAD(d.tile_first, tile_first);
     UPLOAD(d.tile_last, tile_last);
