@@ -123,10 +123,29 @@ def cpu_baseline(cfg: str, runs: int):
                 ms_per_lba=med)
 
 
+def relaunch_distributed(a) -> int:
+    """`--gpus N` (N > 1) without a torch.distributed launcher: start N ranks of this same command
+    under torch.distributed.run (127.0.0.1) as a child process, before anything touches the GPU,
+    and return its exit code."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(a))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s); refusing to report "
+              f"a {world}-rank measurement as {a.gpus} GPUs", file=sys.stderr, flush=True)
+        sys.exit(2)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:

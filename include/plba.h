@@ -138,7 +138,9 @@ int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on);   /* HIP-event timing 
  * [7]=assembly chunks, [8]=edges with a free pose, [9]=point edges, [10]=step hipGraph in use,
  * [11]=sharded code path, [12]=two-sided (twisted) band factorisation, [13]=column-lane
  * band factorisation (bandwidth <= 9), [14]=super-rows of the block-cyclic-reduction
- * factorisation (0 = not used), [15]=dense RCS on the multi-workgroup MFMA path.
+ * factorisation (0 = not used), [15]=dense RCS on the multi-workgroup MFMA path,
+ * [16]=times a block-cyclic-reduction hand-off timed out and the schedule was re-solved with
+ * the column-lane factorisation (the context then keeps that factorisation).
  * Counts are this rank's when the window is sharded. */
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap);
 int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,

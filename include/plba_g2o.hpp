@@ -46,6 +46,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -71,6 +72,51 @@ struct Fixed {
         for (int r = 0; r < R; ++r)
             for (int c = 0; c < C; ++c) assign(e, r, c, 0);
         return e;
+    }
+    // Matrix4d::inverse() of the pose estimate, as the read-back calls it
+    // (src/mapHandler.cpp:6302 `pKFi->T_kf_w = vPose->estimate().inverse();`): the general 4x4
+    // inverse (adjugate / determinant, Eigen's method for fixed 4x4), not a rigid-body shortcut, so a
+    // Tcw whose last row is not exactly (0 0 0 1) inverts the way Eigen would.
+    template <int R_ = R, int C_ = C, typename std::enable_if<R_ == 4 && C_ == 4, int>::type = 0>
+    Fixed inverse() const {
+        const double *m = a;
+        double inv[16];
+        inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] +
+                 m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+        inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] -
+                 m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+        inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] +
+                 m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+        inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] -
+                  m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+        inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] -
+                 m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+        inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] +
+                 m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+        inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] -
+                 m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+        inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] +
+                  m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+        inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] +
+                 m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+        inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] -
+                 m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+        inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] +
+                  m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+        inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] -
+                  m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+        inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] -
+                 m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+        inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] +
+                 m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+        inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] -
+                  m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+        inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] +
+                  m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+        const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+        Fixed o;
+        for (int i = 0; i < 16; ++i) o.a[i] = inv[i] / det;
+        return o;
     }
 
   private:
@@ -131,7 +177,11 @@ struct OptimizableGraph {
         virtual ~Vertex() = default;
         void setId(int id) { id_ = id; }
         int id() const { return id_; }
-        void setFixed(bool f) { fixed_ = f; }
+        // g2o applies a changed fixed flag at the next initializeOptimization/optimize: re-marshal
+        void setFixed(bool f) {
+            if (f != fixed_) structure_changed();
+            fixed_ = f;
+        }
         bool fixed() const { return fixed_; }
         void setMarginalized(bool m) { marg_ = m; }
         bool marginalized() const { return marg_; }
@@ -140,6 +190,7 @@ struct OptimizableGraph {
       protected:
         friend class g2o::SparseOptimizer;
         void touched();            // a host-side estimate changed: re-upload before the next solve
+        void structure_changed();  // fixed flag changed: re-marshal before the next solve
         void sync() const;         // device estimates newer: download
         int id_ = -1, slot_ = -1;  // slot_: index within its kind, assigned by the optimizer
         bool fixed_ = false, marg_ = false;
@@ -148,7 +199,10 @@ struct OptimizableGraph {
     class Edge {
       public:
         virtual ~Edge() { delete rk_; }
-        void setVertex(int i, Vertex *v) { v_[i & 1] = v; }
+        void setVertex(int i, Vertex *v) {
+            if (v != v_[i & 1]) structure_changed();
+            v_[i & 1] = v;
+        }
         Vertex *vertex(int i) const { return v_[i & 1]; }
         void setLevel(int l);
         int level() const { return level_; }
@@ -162,6 +216,7 @@ struct OptimizableGraph {
         void computeError();
         template <class M>
         void setInformation(const M &m) {
+            structure_changed();
             info_ = m(0, 0);
             iso_ = true;
             for (int r = 0; r < dim(); ++r)
@@ -172,6 +227,9 @@ struct OptimizableGraph {
 
       protected:
         friend class g2o::SparseOptimizer;
+        // measurement / information / vertices / camera changed after the window was uploaded:
+        // re-marshal at the next optimize() (g2o reads them at every linearisation)
+        void structure_changed();
         bool depth_ok() const;  // EdgePosePoint::isDepthPositive at the last evaluated state
         Vertex *v_[2] = {nullptr, nullptr};
         RobustKernel *rk_ = nullptr;
@@ -367,10 +425,12 @@ class EdgePosePoint : public g2o::OptimizableGraph::Edge {
     int dim() const override { return 2; }
     template <class V>
     void setMeasurement(const V &m) {
+        structure_changed();
         obs_[0] = m(0);
         obs_[1] = m(1);
     }
     void SetParams(const double &fx, const double &fy, const double &cx, const double &cy) {
+        structure_changed();
         cam_[0] = fx; cam_[1] = fy; cam_[2] = cx; cam_[3] = cy;
     }
     bool isDepthPositive();
@@ -381,9 +441,11 @@ class EdgePoseLine : public g2o::OptimizableGraph::Edge {
     int dim() const override { return 4; }
     template <class V>
     void setMeasurement(const V &m) {
+        structure_changed();
         for (int i = 0; i < 4; ++i) obs_[i] = m(i);
     }
     void SetParams(const double &fx, const double &fy, const double &cx, const double &cy) {
+        structure_changed();
         cam_[0] = fx; cam_[1] = fy; cam_[2] = cx; cam_[3] = cy;
     }
 };
@@ -396,6 +458,12 @@ namespace g2o {
 
 inline void OptimizableGraph::Vertex::touched() {
     if (opt_) opt_->dirty_est_ = true;
+}
+inline void OptimizableGraph::Vertex::structure_changed() {
+    if (opt_) opt_->dirty_struct_ = true;
+}
+inline void OptimizableGraph::Edge::structure_changed() {
+    if (opt_) opt_->dirty_struct_ = true;
 }
 inline void OptimizableGraph::Vertex::sync() const {
     if (opt_ && opt_->dev_newer_) opt_->download();

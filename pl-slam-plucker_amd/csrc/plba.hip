@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/plba.h"
+#include "plba_build.hpp"
 #include "plba_kernels.hpp"
 
 namespace plba {
@@ -79,8 +80,10 @@ struct plba_ctx {
         const void *src;
         bool zero;
         size_t off;
+        const void *dsrc = nullptr;  // device source (copied D2D after the arena is carved)
     };
     std::vector<Item> plan;
+    BuildMem bmemA, bmemB;   // device window build scratch (plba_build.hip), grow-only
     char *arena = nullptr, *staging = nullptr;
     size_t arena_cap = 0, staging_cap = 0;
     Ctrl *h_ctrl = nullptr;  // pinned
@@ -105,6 +108,15 @@ struct plba_ctx {
     int last_steps = 16;     // steps the previous schedule needed (first batch size)
     int cur = 0;             // which state buffer holds the current estimate (mirror of Ctrl::cur)
     bool no_graph = false;   // set when the step cannot be captured (RCCL without capture support)
+    // block cyclic reduction safety net: a BCR hand-off wait that timed out (Ctrl::dev_error)
+    // makes run_schedule restore the schedule's starting state from these copies, switch this
+    // context to the column-lane factorisation for good (no_bcr) and solve the window again
+    bool no_bcr = false;
+    int bcr_fallbacks = 0;
+    int fb_twisted = 0, fb_tw_m = 0;  // the column-lane variant the window falls back to
+    double *bk_T = nullptr, *bk_X = nullptr, *bk_xp = nullptr, *bk_xk = nullptr, *bk_Lpb = nullptr, *bk_XL = nullptr,
+           *bk_xl = nullptr;
+    uint8_t *bk_level = nullptr;
     int steps_launched = 0;
     // kernel timing (optional)
     bool timing = false;
@@ -141,6 +153,8 @@ struct plba_ctx {
         }
         plan.clear();
         d = Dev{};
+        bk_T = bk_X = bk_xp = bk_xk = bk_Lpb = bk_XL = bk_xl = nullptr;
+        bk_level = nullptr;
         uploaded = initialized = false;
     }
     // Records a device array of `count` T (at least 128 bytes: kernels issue unconditional
@@ -153,14 +167,24 @@ struct plba_ctx {
         const size_t sb = count * sizeof(T);
         plan.push_back(Item{(void **)&p, std::max(sb, (size_t)128), src ? sb : 0, src, zero, 0});
     }
+    // a device array filled from device memory (the device window build's outputs)
+    template <typename T>
+    void alloc_dev(T *&p, size_t count, const void *dsrc) {
+        p = nullptr;
+        const size_t sb = count * sizeof(T);
+        plan.push_back(Item{(void **)&p, std::max(sb, (size_t)128), sb, nullptr, false, 0, dsrc});
+    }
     int commit_plan() {
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
         size_t up = 0, tot = 0;
         for (auto &it : plan)
             if (it.src) { it.off = up; up = al(up + it.bytes); }
-        tot = up;
+        size_t dv = up;  // device-sourced arrays after the host-sourced ones, outside the memset
         for (auto &it : plan)
-            if (!it.src) { it.off = tot; tot = al(tot + it.bytes); }
+            if (it.dsrc) { it.off = dv; dv = al(dv + it.bytes); }
+        tot = dv;
+        for (auto &it : plan)
+            if (!it.src && !it.dsrc) { it.off = tot; tot = al(tot + it.bytes); }
         if (tot > arena_cap) {
             (void)hipStreamSynchronize(stream);
             if (arena) (void)hipFree(arena);
@@ -198,7 +222,10 @@ struct plba_ctx {
         // reads of memory no kernel wrote; arrays whose zero start is part of the contract stay 0
         const char *poison = getenv("PLBA_POISON");
         const bool pz = poison && poison[0] == '1';
-        hipError_t e = hipMemsetAsync(arena + up, pz ? 0xFF : 0, tot - up, stream);
+        hipError_t e = hipMemsetAsync(arena + dv, pz ? 0xFF : 0, tot - dv, stream);
+        for (auto &it : plan)
+            if (it.dsrc && it.src_bytes && e == hipSuccess)
+                e = hipMemcpyAsync(arena + it.off, it.dsrc, it.src_bytes, hipMemcpyDeviceToDevice, stream);
         if (e == hipSuccess && pz)
             for (auto &it : plan)
                 if (it.zero && e == hipSuccess) e = hipMemsetAsync(arena + it.off, 0, it.bytes, stream);
@@ -324,10 +351,40 @@ inline int solve_lds_limit() {
 // Factorisation mode of a banded window: PLBA_FACTOR=bcr|cl|band forces one (diagnostics / A-B
 // runs); by default block cyclic reduction once the window has enough super-rows for its
 // log-depth chain to beat the two-sided column-lane chain of (nf+bw)/2 pivot steps.
-inline bool want_bcr(int bw, int nf) {
+inline size_t bcr_back_lds_bytes(int bw) { return sizeof(double) * bcr_back_lds_doubles(bw); }
+template <int... B>
+const void *bcr_back_kernel_impl(int bw, std::integer_sequence<int, B...>) {
+    const void *k = nullptr;
+    ((bw == B ? (k = (const void *)k_rcs_bcr_back<B>, 0) : 0), ...);
+    return k;
+}
+inline const void *bcr_back_kernel(int bw) {
+    return bcr_back_kernel_impl(bw, std::make_integer_sequence<int, kBcrMaxBW + 1>{});
+}
+// Workgroups of the BCR forward kernel the device holds at once: CUs x occupancy (LDS-bound, one
+// per CU above 80 KB). PLBA_BCR_RESIDENT overrides it (tests: force the column-lane choice).
+inline int bcr_resident(int device, int bw) {
+    const char *e = getenv("PLBA_BCR_RESIDENT");
+    if (e && e[0]) return atoi(e);
+    if (bw < 1 || bw > kBcrMaxBW || bcr_lds_bytes(bw) > 159 * 1024) return 0;
+    int cus = 0, occ = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        hipFuncSetAttribute(bcr_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bcr_lds_bytes(bw)) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bcr_kernel(bw), kBcrNT, bcr_lds_bytes(bw)) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return cus * occ;
+}
+// Factorisation mode of a banded window: PLBA_FACTOR=bcr|cl|band forces one (diagnostics / A-B
+// runs); by default block cyclic reduction once the window has enough super-rows for its
+// log-depth chain to beat the two-sided column-lane chain of (nf+bw)/2 pivot steps. BCR only when
+// its N workgroups fit the device at once (`resident`): a launch that cannot hold them all still
+// completes (ticket order, plba_bcr.hpp) but serialises the levels it exists to overlap.
+inline bool want_bcr(int bw, int nf, int resident) {
     if (bw < 1 || bw > kBcrMaxBW) return false;
     const int N = (nf + bw - 1) / bw;
-    if (N < 2 || N > kBcrMaxRows || bcr_lds_bytes(bw) > 159 * 1024) return false;
+    if (N < 2 || N > resident || bcr_lds_bytes(bw) > 159 * 1024) return false;
     const char *f = getenv("PLBA_FACTOR");
     if (f && f[0]) return std::string(f) == "bcr";
     // latency model calibrated on C3/C4/C5 (profiles/r02): the two-sided column-lane
@@ -341,8 +398,9 @@ inline bool want_bcr(int bw, int nf) {
 }
 inline void launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
-    if (d.bcr) {
+    if (d.bcr) {  // forward elimination, then back substitution + pose update (plba_bcr.hpp)
         (void)hipLaunchKernel(bcr_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrNT), args, bcr_lds_bytes(d.bw), s);
+        (void)hipLaunchKernel(bcr_back_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrBackNT), args, bcr_back_lds_bytes(d.bw), s);
         return;
     }
     if (d.cl) {
@@ -516,16 +574,22 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ctx->set_error("null array in graph");
         return PLBA_E_INVALID;
     }
-    for (int e = 0; e < g->n_ept; ++e)
-        if (g->ept_lm[e] < 0 || g->ept_lm[e] >= g->n_pt || g->ept_kf[e] < 0 || g->ept_kf[e] >= g->n_kf) {
-            ctx->set_error("point edge %d references a missing vertex", e);
-            return PLBA_E_INVALID;
-        }
-    for (int e = 0; e < g->n_eln; ++e)
-        if (g->eln_lm[e] < 0 || g->eln_lm[e] >= g->n_ln || g->eln_kf[e] < 0 || g->eln_kf[e] >= g->n_kf) {
-            ctx->set_error("line edge %d references a missing vertex", e);
-            return PLBA_E_INVALID;
-        }
+    // Window structure on the device (plba_build.hip: sorts / scans / scatters on the solver
+    // stream) unless PLBA_HOST_BUILD=1 (the host build below, kept as the reference the device
+    // build is tested against bit for bit, and for windows whose envelope needs the RCM order).
+    const bool devb_wanted = g->n_kf > 0 && !env_flag("PLBA_HOST_BUILD");
+    if (!devb_wanted) {  // (the device build validates the edges itself)
+        for (int e = 0; e < g->n_ept; ++e)
+            if (g->ept_lm[e] < 0 || g->ept_lm[e] >= g->n_pt || g->ept_kf[e] < 0 || g->ept_kf[e] >= g->n_kf) {
+                ctx->set_error("point edge %d references a missing vertex", e);
+                return PLBA_E_INVALID;
+            }
+        for (int e = 0; e < g->n_eln; ++e)
+            if (g->eln_lm[e] < 0 || g->eln_lm[e] >= g->n_ln || g->eln_kf[e] < 0 || g->eln_kf[e] >= g->n_kf) {
+                ctx->set_error("line edge %d references a missing vertex", e);
+                return PLBA_E_INVALID;
+            }
+    }
     auto tmark = std::chrono::steady_clock::now();
     auto mark = [&](const char *what) {
         const auto t = std::chrono::steady_clock::now();
@@ -539,6 +603,59 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     const int R = ctx->comm.nranks, rank = ctx->comm.rank;
     ctx->n_kf = n_kf; ctx->n_pt = n_pt_g; ctx->n_ln = n_ln_g; ctx->Ep = Ep_g; ctx->El = El_g;
 
+    std::vector<int32_t> lm_gpos, kf_hidx, first_blk, e_lm, e_kf, e_hidx, e_orig, e_gpos, lm_off, pe_off, pe_list;
+    std::vector<double> e_obs, e_info;
+    int n_pt = 0, n_ln = 0, Ep = 0, El = 0, nf = 0, bw = 0;
+    WindowBuild wb;
+    bool devb = false;
+    if (devb_wanted) {
+        // free poses by vertex id (buildIndexMapping) and the id rank of every keyframe
+        std::vector<int32_t> korder(n_kf), kpos(n_kf);
+        std::iota(korder.begin(), korder.end(), 0);
+        std::stable_sort(korder.begin(), korder.end(), [&](int a, int b) { return g->kf_id[a] < g->kf_id[b]; });
+        kf_hidx.assign(n_kf, -1);
+        for (int i = 0; i < n_kf; ++i) {
+            kpos[korder[i]] = i;
+            if (!g->kf_fixed[korder[i]]) kf_hidx[korder[i]] = nf++;
+        }
+        wb.g = g;
+        wb.nranks = R;
+        wb.rank = rank;
+        wb.nf = nf;
+        wb.kf_hidx = kf_hidx.data();
+        wb.kpos = kpos.data();
+        wb.stream = ctx->stream;
+        char msg[256] = {0};
+        const int brc = build_stage1(ctx->bmemA, wb, msg, sizeof msg);
+        if (brc) {
+            ctx->set_error("%s", msg);
+            return brc;
+        }
+        first_blk = wb.first_blk;
+        for (int h = 0; h < nf; ++h) bw = std::max(bw, h - first_blk[h]);
+        // an envelope the banded kernels cannot take may narrow under the RCM order: host build
+        devb = !(bw > kClMaxBW && nf > 2 && !env_flag("PLBA_NO_RCM"));
+        if (devb) {
+            n_pt = wb.n_pt; n_ln = wb.n_ln; Ep = wb.Ep; El = wb.El;
+            ctx->n_free_edges = wb.n_free_edges;
+            // host mirrors of the output maps (plba_download / plba_get_edge_chi2)
+            lm_gpos.resize(wb.n_lm);
+            e_orig.resize(wb.E);
+            if (wb.n_lm)
+                PLBA_CHECK(hipMemcpyAsync(lm_gpos.data(), wb.lm_gpos, sizeof(int32_t) * wb.n_lm, hipMemcpyDeviceToHost, ctx->stream));
+            if (wb.E)
+                PLBA_CHECK(hipMemcpyAsync(e_orig.data(), wb.e_orig, sizeof(int32_t) * wb.E, hipMemcpyDeviceToHost, ctx->stream));
+            PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+            ctx->lm_gpos = lm_gpos;
+            ctx->e_orig = e_orig;
+            ctx->h_level.assign(wb.E, 0);
+        } else {
+            bw = 0;
+            nf = 0;
+        }
+        mark("device build (stage 1)");
+    }
+    if (!devb) {
     // landmarks owned by this rank (all of them unless the window is sharded)
     std::vector<int32_t> pt_owner(n_pt_g, 0), ln_owner(n_ln_g, 0);
     if (R > 1) shard_plan(g, R, pt_owner.data(), ln_owner.data());
@@ -546,8 +663,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // keyframe of their first observation, so the edges of one pose — and the landmarks one RCS
     // block couples — sit in a narrow range of the landmark-major edge array (cache locality of
     // the pose reduction and the Schur assembly; any order gives the same solution).
-    std::vector<int32_t> pt_loc(n_pt_g, -1), ln_loc(n_ln_g, -1), lm_gpos;
-    int n_pt = 0, n_ln = 0;
+    std::vector<int32_t> pt_loc(n_pt_g, -1), ln_loc(n_ln_g, -1);
+    lm_gpos.clear();
     {
         std::vector<int32_t> korder_(n_kf), kpos(n_kf);
         std::iota(korder_.begin(), korder_.end(), 0);
@@ -577,7 +694,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         order(n_ln_g, ln_owner, key_ln, ln_loc, n_ln, n_pt_g);
     }
     ctx->lm_gpos = lm_gpos;
-    int Ep = 0, El = 0;
     for (int e = 0; e < Ep_g; ++e) Ep += pt_loc[g->ept_lm[e]] >= 0;
     for (int e = 0; e < El_g; ++e) El += ln_loc[g->eln_lm[e]] >= 0;
     const int n_lm = n_pt + n_ln, E = Ep + El;
@@ -586,11 +702,10 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     std::vector<int32_t> korder(n_kf);
     std::iota(korder.begin(), korder.end(), 0);
     std::stable_sort(korder.begin(), korder.end(), [&](int a, int b) { return g->kf_id[a] < g->kf_id[b]; });
-    std::vector<int32_t> kf_hidx(n_kf, -1);
-    int nf = 0;
+    kf_hidx.assign(n_kf, -1);
     for (int k : korder)
         if (!g->kf_fixed[k]) kf_hidx[k] = nf++;
-    std::vector<int32_t> first_blk(nf);
+    first_blk.assign(nf, 0);
     auto envelope = [&](const std::vector<int32_t> &hidx, std::vector<int32_t> &fb) {
         for (int h = 0; h < nf; ++h) fb[h] = h;
         std::vector<int32_t> lmin(n_pt_g + n_ln_g, INT32_MAX);
@@ -614,7 +729,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         for (int h = 0; h < nf; ++h) w = std::max(w, h - fb[h]);
         return w;
     };
-    int bw = envelope(kf_hidx, first_blk);
+    bw = envelope(kf_hidx, first_blk);
     // Reverse Cuthill–McKee on the free-pose coupling graph when the natural (id) order leaves an
     // envelope wider than the column-lane / BCR kernels take: windows that revisit old keyframes
     // couple poses a loop apart. LinearSolverEigen orders the same matrix by AMD; any symmetric
@@ -639,11 +754,11 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         if (pt_loc[g->ept_lm[e]] >= 0) lm_cnt[pt_loc[g->ept_lm[e]] + 1]++;
     for (int e = 0; e < El_g; ++e)
         if (ln_loc[g->eln_lm[e]] >= 0) lm_cnt[n_pt + ln_loc[g->eln_lm[e]] + 1]++;
-    std::vector<int32_t> lm_off(n_lm + 1, 0);
+    lm_off.assign(n_lm + 1, 0);
     for (int l = 0; l < n_lm; ++l) lm_off[l + 1] = lm_off[l] + lm_cnt[l + 1];
     std::vector<int32_t> fill(lm_off.begin(), lm_off.end() - 1);
-    std::vector<int32_t> e_lm(E), e_kf(E), e_hidx(E), e_orig(E), e_gpos(E);
-    std::vector<double> e_obs((size_t)E * 4, 0.0), e_info(E);
+    e_lm.assign(E, 0); e_kf.assign(E, 0); e_hidx.assign(E, 0); e_orig.assign(E, 0); e_gpos.assign(E, 0);
+    e_obs.assign((size_t)E * 4, 0.0); e_info.assign(E, 0.0);
     for (int e = 0; e < Ep_g; ++e) {
         const int l = pt_loc[g->ept_lm[e]];
         if (l < 0) continue;
@@ -673,16 +788,18 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 
     mark("landmark order + CSR");
     // free-pose-major edge lists (ascending CSR edge index)
-    std::vector<int32_t> pe_off(nf + 1, 0);
+    pe_off.assign(nf + 1, 0);
     for (int e = 0; e < E; ++e)
         if (e_hidx[e] >= 0) pe_off[e_hidx[e] + 1]++;
     for (int h = 0; h < nf; ++h) pe_off[h + 1] += pe_off[h];
-    std::vector<int32_t> pe_list(pe_off[nf]);
+    pe_list.assign(pe_off[nf], 0);
     {
         std::vector<int32_t> f(pe_off.begin(), pe_off.end() - 1);
         for (int e = 0; e < E; ++e)
             if (e_hidx[e] >= 0) pe_list[f[e_hidx[e]]++] = e;
     }
+    }  // host build
+    const int n_lm = n_pt + n_ln, E = Ep + El;
 
     // Reduced-camera block pattern: the envelope of the lower triangle. first_blk[i2] = the lowest
     // free pose sharing a landmark with free pose i2, over the WHOLE window on every rank (the
@@ -706,7 +823,16 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             blk_i1[b] = i1;
             blk_i2[b] = h;
         }
-    {
+    if (devb) {  // device build, stage 2: Schur triples sorted by block on the device
+        char msg[256] = {0};
+        const int brc = build_stage2(ctx->bmemA, ctx->bmemB, wb, blk_base, nblk, msg, sizeof msg);
+        if (brc) {
+            ctx->set_error("%s", msg);
+            return brc;
+        }
+        blk_off = wb.h_blk_off;
+        ctx->n_triples = (size_t)wb.n_triples;
+    } else {
         auto for_pairs = [&](auto &&f) {
             for (int l = 0; l < n_lm; ++l)
                 for (int a = lm_off[l]; a < lm_off[l + 1]; ++a) {
@@ -784,13 +910,18 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // two-sided factorisation when the chain is long enough to halve and the separator's dense
     // system fits next to the band window in LDS (PLBA_NO_TWIST=1 disables, diagnostics only)
     const char *no_twist = getenv("PLBA_NO_TWIST");
-    const bool bcr = band_mode && want_bcr(bw, nf);
+    const bool bcr = band_mode && !ctx->no_bcr && want_bcr(bw, nf, bcr_resident(ctx->opts.device, bw));
     d.bcr = bcr ? 1 : 0;
     d.bcr_N = bcr ? (nf + bw - 1) / bw : 0;
     const bool cl = band_mode && !bcr && use_cl(bw);
     const bool twisted = band_mode && !bcr && bw >= 1 && nf >= 2 * bw + 16 &&
                          (cl ? cl_lds_bytes(bw, nf, true) : twisted_lds_bytes(bw, nf)) <= 159 * 1024 &&
                          !(no_twist && no_twist[0] == '1');
+    // the column-lane factorisation a BCR window falls back to (run_schedule) and its arrays
+    const bool fb_tw = bcr && use_cl(bw) && nf >= 2 * bw + 16 && cl_lds_bytes(bw, nf, true) <= 159 * 1024 &&
+                       !(no_twist && no_twist[0] == '1');
+    ctx->fb_twisted = fb_tw ? 1 : 0;
+    ctx->fb_tw_m = fb_tw ? (nf - bw) / 2 : 0;
     d.cl = cl && cl_lds_bytes(bw, nf, twisted) <= 159 * 1024 ? 1 : 0;
     d.twisted = twisted ? 1 : 0;
     d.tw_m = twisted ? (nf - bw) / 2 : 0;
@@ -809,13 +940,15 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.n_lms_blocks = blocks_for(n_lm * kLmLanes, kLmsNT);
     d.n_kf_blocks = blocks_for(n_kf);
 
-    std::vector<double> T((size_t)n_kf * 12), X((size_t)n_lm * 4, 0.0);
-    for (size_t i = 0; i < T.size(); ++i) T[i] = g->kf_Tcw[i];
-    for (int p = 0; p < n_pt; ++p)
-        for (int k = 0; k < 3; ++k) X[(size_t)p * 4 + k] = g->pt_xyz[3 * (size_t)lm_gpos[p] + k];
-    for (int l = 0; l < n_ln; ++l)
-        for (int k = 0; k < 4; ++k)
-            X[(size_t)(n_pt + l) * 4 + k] = g->ln_orth[4 * (size_t)(lm_gpos[n_pt + l] - n_pt_g) + k];
+    std::vector<double> T(g->kf_Tcw, g->kf_Tcw + (size_t)n_kf * 12), X;
+    if (!devb) {
+        X.assign((size_t)n_lm * 4, 0.0);
+        for (int p = 0; p < n_pt; ++p)
+            for (int k = 0; k < 3; ++k) X[(size_t)p * 4 + k] = g->pt_xyz[3 * (size_t)lm_gpos[p] + k];
+        for (int l = 0; l < n_ln; ++l)
+            for (int k = 0; k < 4; ++k)
+                X[(size_t)(n_pt + l) * 4 + k] = g->ln_orth[4 * (size_t)(lm_gpos[n_pt + l] - n_pt_g) + k];
+    }
 
     std::vector<int32_t> h_kf(bcr ? nf : 0, 0);
     for (int k = 0; k < n_kf && bcr; ++k)
@@ -824,12 +957,18 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 #define ALLOC(p, n_) ctx->alloc(p, (size_t)(n_))
 #define ZALLOC(p, n_) ctx->alloc(p, (size_t)(n_), nullptr, true)
 #define UPLOAD(p, v) ctx->alloc(p, (v).size(), (v).data())
+// host vector (host build) or the device build's array of n_ elements
+#define UPLOAD_D(p, v, dptr, n_)                           \
+    do {                                                  \
+        if (devb) ctx->alloc_dev(p, (size_t)(n_), (dptr)); \
+        else UPLOAD(p, v);                                \
+    } while (0)
     UPLOAD(d.T_init, T);
     UPLOAD(d.Tb[0], T);
     ALLOC(d.Tb[1], T.size());
-    UPLOAD(d.X_init, X);
-    UPLOAD(d.Xb[0], X);
-    ALLOC(d.Xb[1], X.size());
+    UPLOAD_D(d.X_init, X, wb.X, (size_t)n_lm * 4);
+    UPLOAD_D(d.Xb[0], X, wb.X, (size_t)n_lm * 4);
+    ALLOC(d.Xb[1], (size_t)n_lm * 4);
     ALLOC(d.xk[0], (size_t)n_kf * 6);
     ALLOC(d.xk[1], (size_t)n_kf * 6);
     // hand-rolled GBA: endpoint lines in the reference's (global) order, their 6x6 blocks
@@ -843,17 +982,17 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.Lpb[0], (size_t)std::max(n_ln, 1) * 8);
     ALLOC(d.Lpb[1], (size_t)std::max(n_ln, 1) * 8);
     UPLOAD(d.kf_hidx, kf_hidx);
-    UPLOAD(d.e_lm, e_lm);
-    UPLOAD(d.e_kf, e_kf);
-    UPLOAD(d.e_hidx, e_hidx);
-    UPLOAD(d.e_obs, e_obs);
-    UPLOAD(d.e_info, e_info);
+    UPLOAD_D(d.e_lm, e_lm, wb.e_lm, E);
+    UPLOAD_D(d.e_kf, e_kf, wb.e_kf, E);
+    UPLOAD_D(d.e_hidx, e_hidx, wb.e_hidx, E);
+    UPLOAD_D(d.e_obs, e_obs, wb.e_obs, (size_t)E * 4);
+    UPLOAD_D(d.e_info, e_info, wb.e_info, E);
     ZALLOC(d.e_level, E);
     ALLOC(d.e_active, E);
-    UPLOAD(d.lm_off, lm_off);
+    UPLOAD_D(d.lm_off, lm_off, wb.lm_off, n_lm + 1);
     ALLOC(d.lm_active, n_lm);
-    UPLOAD(d.pe_off, pe_off);
-    UPLOAD(d.pe_list, pe_list);
+    UPLOAD_D(d.pe_off, pe_off, wb.pe_off, nf + 1);
+    UPLOAD_D(d.pe_list, pe_list, wb.pe_list, ctx->n_free_edges);
     ALLOC(d.A, (size_t)E * 12);
     ALLOC(d.cvec, (size_t)E * 2);
     ALLOC(d.B, (size_t)E * 8);
@@ -869,7 +1008,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.blk_i1, blk_i1);
     UPLOAD(d.blk_i2, blk_i2);
     UPLOAD(d.blk_off, blk_off);
-    UPLOAD(d.trip, trip);
+    UPLOAD_D(d.trip, trip, wb.trip, 2 * (size_t)ctx->n_triples);
     d.nch = nch;
     UPLOAD(d.ch_blk, ch_blk);
     UPLOAD(d.ch_off, ch_off);
@@ -883,7 +1022,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.Lband, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
     ALLOC(d.Kinv, (size_t)nf * 36);
     ALLOC(d.zb, (size_t)nf * 6);
-    if (twisted) {
+    if (twisted || fb_tw) {
         ZALLOC(d.Bd2, (size_t)nf * (bw + 1) * 36);
         ALLOC(d.bs2, (size_t)nf * 6);
         ALLOC(d.Lband2, (size_t)nf * (bw + 1) * 36);
@@ -896,10 +1035,20 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate
         ALLOC(d.bcr_pub, (size_t)d.bcr_N * bcr_pub_doubles(bw));
         ALLOC(d.bcr_x, (size_t)d.bcr_N * bcr_xrec(bw));
+        ALLOC(d.bcr_X, (size_t)d.bcr_N * bcr_X_doubles(bw));
         UPLOAD(d.h_kf, h_kf);
         ZALLOC(d.bcr_flag, 2 * (size_t)d.bcr_N);
-        ZALLOC(d.bcr_ctl, 4);
+        ZALLOC(d.bcr_ctl, kBcrCtl);
         ZALLOC(d.bcr_stamps, (size_t)d.bcr_N * kBcrStamps);
+        // the schedule's starting state, restored if a hand-off wait times out (run_schedule)
+        ctx->alloc(ctx->bk_T, (size_t)n_kf * 12);
+        ctx->alloc(ctx->bk_X, (size_t)std::max(n_lm, 1) * 4);
+        ctx->alloc(ctx->bk_xp, (size_t)std::max(n, 6));
+        ctx->alloc(ctx->bk_xk, (size_t)n_kf * 6);
+        ctx->alloc(ctx->bk_Lpb, (size_t)std::max(n_ln, 1) * 8);
+        ctx->alloc(ctx->bk_XL, (size_t)std::max(n_ln_g, 1) * 6);
+        ctx->alloc(ctx->bk_level, (size_t)std::max(E, 1));
+        ctx->alloc(ctx->bk_xl, (size_t)std::max(n_lm, 1) * 4);
     }
     if (!band_mode) ZALLOC(d.bcr_stamps, kBcrStamps);  // dense-path phase stamps (PLBA_DIAG bit 8)
     ALLOC(d.bs, n);
@@ -929,11 +1078,11 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.red_dec, 2);
     if (sharded) {
         ALLOC(d.red_rcs_loc, (size_t)nblk * 36 + (size_t)nf * 6);
-        ALLOC(d.red_dec_loc, 2);
+        ALLOC(d.red_dec_loc, 3);  // + the hand-off error agreement slot (agree_dev_error)
     }
     if (sharded) {  // final gather of the full window: X | χ² | depth | level
         UPLOAD(d.lm_gpos, lm_gpos);
-        UPLOAD(d.e_gpos, e_gpos);
+        UPLOAD_D(d.e_gpos, e_gpos, wb.e_gpos, E);
         ALLOC(d.gat, (size_t)(n_pt_g + n_ln_g) * 4 + 3 * (size_t)(Ep_g + El_g));
     }
 #ifdef PLBA_STAMPS
@@ -942,6 +1091,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 #undef ALLOC
 #undef ZALLOC
 #undef UPLOAD
+#undef UPLOAD_D
     mark("host arrays staged");
     int rc = ctx->commit_plan();
     if (rc) return rc;
@@ -954,7 +1104,18 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.pact_w = d.red_iter_loc + (size_t)nf * 42;
     if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)band_lds_bytes(bw, nf)));
-    if (bcr) PLBA_CHECK(hipFuncSetAttribute(bcr_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bcr_lds_bytes(bw)));
+    if (bcr) {
+        PLBA_CHECK(hipFuncSetAttribute(bcr_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bcr_lds_bytes(bw)));
+        PLBA_CHECK(hipFuncSetAttribute(bcr_back_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)bcr_back_lds_bytes(bw)));
+        if (fb_tw) {
+            const void *k = cl_kernel_impl(bw, true, std::make_integer_sequence<int, kClMaxBW + 1>{});
+            PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, true)));
+        } else {
+            const void *k = cl_kernel_impl(bw, false, std::make_integer_sequence<int, kClMaxBW + 1>{});
+            PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, false)));
+        }
+    }
     if (d.cl) {  // the column-lane kernel's LDS grows with nf (x_p staging of the two-sided variant)
         const void *k = cl_kernel_impl(bw, twisted, std::make_integer_sequence<int, kClMaxBW + 1>{});
         PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, twisted)));
@@ -1119,9 +1280,62 @@ int read_ctrl(plba_ctx *ctx) {
     return PLBA_OK;
 }
 
+void destroy_graphs(plba_ctx *ctx) {
+    if (ctx->step_exec) (void)hipGraphExecDestroy(ctx->step_exec);
+    if (ctx->step_graph) (void)hipGraphDestroy(ctx->step_graph);
+    ctx->step_exec = nullptr;
+    ctx->step_graph = nullptr;
+    for (int i = 0; i < plba_ctx::kMultiLevels; ++i) {
+        if (ctx->multi_exec[i]) (void)hipGraphExecDestroy(ctx->multi_exec[i]);
+        if (ctx->multi_graph[i]) (void)hipGraphDestroy(ctx->multi_graph[i]);
+        ctx->multi_exec[i] = nullptr;
+        ctx->multi_graph[i] = nullptr;
+    }
+}
+
+// Copies of the state a schedule starts from (BCR windows only): save = true before the first
+// batch, save = false to put it back after a hand-off timeout.
+int bcr_state_copy(plba_ctx *ctx, bool save) {
+    Dev &d = ctx->d;
+    const int c = ctx->cur;
+    hipStream_t s = ctx->stream;
+    auto cp = [&](void *bk, void *live, size_t bytes) -> hipError_t {
+        if (!bytes) return hipSuccess;
+        return save ? hipMemcpyAsync(bk, live, bytes, hipMemcpyDeviceToDevice, s)
+                    : hipMemcpyAsync(live, bk, bytes, hipMemcpyDeviceToDevice, s);
+    };
+    PLBA_CHECK(cp(ctx->bk_T, d.Tb[c], sizeof(double) * (size_t)d.n_kf * 12));
+    PLBA_CHECK(cp(ctx->bk_X, d.Xb[c], sizeof(double) * (size_t)d.n_lm * 4));
+    PLBA_CHECK(cp(ctx->bk_xp, d.xp, sizeof(double) * (size_t)d.n));
+    PLBA_CHECK(cp(ctx->bk_xk, d.xk[c], sizeof(double) * (size_t)d.n_kf * 6));
+    PLBA_CHECK(cp(ctx->bk_Lpb, d.Lpb[c], sizeof(double) * (size_t)d.n_ln * 8));
+    PLBA_CHECK(cp(ctx->bk_XL, d.XL[c], sizeof(double) * (size_t)ctx->n_ln * 6));
+    PLBA_CHECK(cp(ctx->bk_level, d.e_level, (size_t)d.E));
+    PLBA_CHECK(cp(ctx->bk_xl, d.xl, sizeof(double) * (size_t)d.n_lm * 4));
+    return PLBA_OK;
+}
+
+// Sharded windows: every rank learns whether any rank hit a hand-off timeout in this batch, so
+// that all of them fall back together (a collective cannot be re-run by one rank alone).
+int agree_dev_error(plba_ctx *ctx, int mine, int *any) {
+    *any = mine;
+    if (!ctx->d.sharded) return PLBA_OK;
+    double *buf = ctx->d.red_dec_loc + 2;  // spare slot after the two decision sums
+    const double v = mine ? 1.0 : 0.0;
+    PLBA_CHECK(hipMemcpyAsync(buf, &v, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    int rc = allreduce(ctx, buf, buf, 1);
+    if (rc) return rc;
+    double out = 0.0;
+    PLBA_CHECK(hipMemcpyAsync(&out, buf, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    *any = out != 0.0 ? 1 : 0;
+    return PLBA_OK;
+}
+
 // Run a schedule of 1 or 2 optimize() calls entirely on the device: replay the step graph in
 // batches, polling the control block once per batch.
-int run_schedule(plba_ctx *ctx, const Ctrl &init) {
+int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
+    dev_error = false;
     Dev &d = ctx->d;
     *ctx->h_ctrl = init;
     PLBA_CHECK(hipMemcpyAsync(d.ctrl, ctx->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, ctx->stream));
@@ -1161,8 +1375,11 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
         launched += batch;
         int rc = read_ctrl(ctx);
         if (rc) return rc;
-        if (ctx->h_ctrl->dev_error) {
-            ctx->set_error("a bounded in-kernel hand-off wait timed out (workgroups not co-resident?)");
+        int any_error = ctx->h_ctrl->dev_error;
+        if (d.sharded && d.bcr && (rc = agree_dev_error(ctx, any_error, &any_error))) return rc;
+        if (any_error) {
+            dev_error = true;
+            ctx->set_error("a bounded in-kernel hand-off wait timed out");
             return PLBA_E_DEVICE;
         }
         if (ctx->h_ctrl->all_done) break;
@@ -1182,6 +1399,35 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     if (nt) PLBA_CHECK(hipMemcpy(tr.data(), d.trace, sizeof(plba_iter_trace) * nt, hipMemcpyDeviceToHost));
     ctx->trace.insert(ctx->trace.end(), tr.begin(), tr.end());
     return PLBA_OK;
+}
+
+// run_schedule_once with the BCR safety net: the starting state is copied first; if a hand-off
+// wait times out (Ctrl::dev_error — every later kernel of that batch is a no-op), the state is put
+// back, the window is switched to the column-lane factorisation for the rest of this context's
+// life (its arrays were allocated with the BCR ones) and the same schedule runs again, in this
+// process. Sharded windows agree on the error first, so every rank falls back together.
+int run_schedule(plba_ctx *ctx, const Ctrl &init) {
+    Dev &d = ctx->d;
+    int rc;
+    if (d.bcr && (rc = bcr_state_copy(ctx, true))) return rc;
+    bool dev_error = false;
+    rc = run_schedule_once(ctx, init, dev_error);
+    if (!rc || !dev_error || !d.bcr) return rc;
+    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    if ((rc = bcr_state_copy(ctx, false))) return rc;
+    if (ctx->opts.verbose)
+        fprintf(stderr, "[plba] BCR hand-off timed out; re-solving with the column-lane factorisation\n");
+    destroy_graphs(ctx);
+    d.bcr = 0;
+    d.bcr_N = 0;
+    d.cl = 1;
+    d.twisted = ctx->fb_twisted;
+    d.tw_m = ctx->fb_tw_m;
+    ctx->no_bcr = true;
+    ++ctx->bcr_fallbacks;
+    ctx->err.clear();
+    rc = run_schedule_once(ctx, init, dev_error);
+    return rc;
 }
 
 Ctrl schedule_init(plba_ctx *ctx, int n_stages) {
@@ -1285,6 +1531,8 @@ int plba_destroy(plba_ctx *ctx) {
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
     if (ctx->pgo_mem) (void)hipFree(ctx->pgo_mem);
+    ctx->bmemA.release();
+    ctx->bmemB.release();
     if (ctx->pgo_hout) (void)hipHostFree(ctx->pgo_hout);
     if (ctx->comm.hbuf) (void)hipHostFree(ctx->comm.hbuf);
     if (ctx->comm.nccl) (void)ncclCommDestroy(ctx->comm.nccl);
@@ -1657,11 +1905,11 @@ int plba_debug_bcr_stamps(plba_ctx *ctx, unsigned long long *out, int32_t cap, i
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[16] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+    const int64_t v[17] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
                            ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N,
-                           ctx->d.dense_mfma};
-    for (int i = 0; i < cap && i < 16; ++i) out[i] = v[i];
+                           ctx->d.dense_mfma, ctx->bcr_fallbacks};
+    for (int i = 0; i < cap && i < 17; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

@@ -19,25 +19,65 @@
 // The survivors pick up their neighbours' contributions level by level (fixed order: above,
 // then below, level by level — results do not depend on timing).
 //
+// Two launches per factorisation, each workgroup taking its super-row from a ticket counter:
+//   k_rcs_factor_bcr  forward elimination, tickets in increasing level order (level 0 rows, then
+//                     level 1, ..., the root last). A row waits only for rows of lower levels, whose
+//                     tickets were taken earlier by workgroups that are running and never wait on a
+//                     later ticket, so the launch completes whatever the co-residency (a workgroup
+//                     that cannot be resident yet holds no ticket anybody waits for). Each row stores
+//                     X = D_m⁻¹[U | V | b] for the backward pass; the root solves x_0.
+//   k_rcs_bcr_back    back substitution x_m = X_b - X_U x_a - X_V x_c, tickets in decreasing level
+//                     order (root first): a row waits only for rows of higher levels (earlier
+//                     tickets). Then the pose update of the row's poses.
+//
 // Hand-offs (MI355X_MICROARCH.md, "Valid forms" table row 1): payload stored write-through
 // (sc1, __hip_atomic_store relaxed/agent), every storing wave drains vmcnt, workgroup barrier,
 // ONE lane stores the flag (relaxed agent atomic); the consumer polls the flag from one lane,
 // barrier, then every load of the payload is an sc1 load (__hip_atomic_load relaxed/agent).
-// Flags carry an epoch (launch count + 1) kept in bcr_ctl[0], advanced by the last workgroup
-// to finish (arrival counter), so nothing has to be cleared between launches or graph replays.
-// Every spin is bounded; a timeout raises Ctrl::dev_error (reported as PLBA_E_DEVICE).
+// Flags carry an epoch (factorisation count + 1) kept in bcr_ctl[0], advanced by the last
+// workgroup of the backward launch (arrival counter), so nothing has to be cleared between launches
+// or graph replays. bcr_ctl: [0] epoch, [1] forward arrivals, [2] forward tickets, [3] backward
+// arrivals, [4] backward tickets. Every spin is bounded; a timeout raises Ctrl::dev_error, which
+// stops every later kernel of the batch (the guards) and makes the host re-solve the window with
+// the column-lane factorisation (plba.hip, run_schedule).
 //
 // Reference semantics: LinearSolverEigen = SimplicialLDLT fails iff a pivot
 // is exactly 0. Every 6x6 pivot block is factorised LDLᵀ without pivoting, so its scalar pivots
 // are LDLᵀ pivots of the (reordered) system and a zero one fails the solve; x_p then keeps its
 // previous value (g2o still calls update()).
 //
-// Requires all N workgroups to be co-resident (one per CU, N <= kBcrMaxRows).
+// Co-residency of the N workgroups is not required for completion (tickets above); the host
+// selects BCR only when the N workgroups fit the device at once (occupancy x CUs), since a
+// partly serialised launch loses the log-depth chain it is chosen for.
 
 constexpr int kBcrNT = 512;
 constexpr int kBcrMaxBW = 9;
 constexpr int kBcrMaxRows = 240;   // co-residency margin below the 256 CUs
 constexpr int kBcrParts = 12;      // partial sums per row of the x_m mat-vec
+constexpr int kBcrBackNT = 256;    // backward (back substitution + pose update) workgroup
+constexpr int kBcrCtl = 8;         // bcr_ctl words
+
+// super-row of a forward ticket: level 0 rows (odd m) in increasing m, then level 1 (m ≡ 2 mod 4),
+// ..., the root (m = 0, level L = ceil(log2 N)) last. Level l holds the m = 2^l (2i + 1) < N.
+__device__ __forceinline__ int bcr_row_fwd(int t, int N, int L) {
+    for (int l = 0; l < L; ++l) {
+        const int cnt = (((N - 1) >> l) + 1) >> 1;
+        if (t < cnt) return (2 * t + 1) << l;
+        t -= cnt;
+    }
+    return 0;
+}
+// super-row of a backward ticket: the root first, then level L-1, ..., level 0
+__device__ __forceinline__ int bcr_row_bwd(int t, int N, int L) {
+    if (t == 0) return 0;
+    --t;
+    for (int l = L - 1; l >= 0; --l) {
+        const int cnt = (((N - 1) >> l) + 1) >> 1;
+        if (t < cnt) return (2 * t + 1) << l;
+        t -= cnt;
+    }
+    return 0;
+}
 
 __host__ __device__ constexpr int bcr_tri(int bw) { return bw * (bw + 1) / 2; }
 // Gram tiles: lower triangle of (2bw+1)x(2bw+1) 6x6 blocks over [U | V | b], minus the (b,b) corner
@@ -52,17 +92,26 @@ __host__ __device__ constexpr size_t bcr_lds_doubles(int bw) {
 // published record of an eliminated super-row, element-major for coalesced write-through
 // stores: [36][ngram] Gram tiles (F = A(c,a) tiles stored negated) + 1 failure word
 __host__ __device__ constexpr size_t bcr_pub_doubles(int bw) { return (size_t)36 * bcr_ngram(bw) + 2; }
-// solution record of a super-row: x (6 bw) + failure word (propagated down the back substitution)
+// solution record of a super-row: x (6 bw), padded
 __host__ __device__ constexpr int bcr_xrec(int bw) { return 6 * bw + 2; }
+// X = D_m⁻¹ [U | V | b] of an eliminated super-row, [6 bw][12 bw + 1] row-major
+__host__ __device__ constexpr size_t bcr_X_doubles(int bw) { return (size_t)(6 * bw) * (12 * bw + 1); }
+// backward kernel LDS: X_m | x_a | x_c | x_m | mat-vec partials | poses [bw][24] + λ
+__host__ __device__ constexpr size_t bcr_back_lds_doubles(int bw) {
+    return bcr_X_doubles(bw) + 3 * (size_t)(6 * bw) + (size_t)kBcrParts * (6 * bw) + (size_t)bw * 24 + 2;
+}
 
 // one lane: relaxed poll until the flag carries `epoch`; bounded (~0.3 s), timeout -> *err = 1.
-// PLBA_DIAG bit 64 (failure-path test only): the flag is checked once, so every hand-off that
-// is not already published times out and the solve must come back as PLBA_E_DEVICE
+// PLBA_DIAG bit 64 (failure-path test only): every wait times out at once, so the first hand-off
+// of a launch raises the error and the host's fallback must take over
 __device__ __forceinline__ bool bcr_poll(uint32_t *flag, uint32_t epoch, int32_t *err, int diag) {
-    const uint32_t lim = (diag & 64) ? 0u : (1u << 23);
+    if (diag & 64) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+    }
     for (uint32_t spins = 0;; ++spins) {
         if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return true;
-        if (spins >= lim) {
+        if (spins >= (1u << 23)) {
             __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
@@ -144,7 +193,7 @@ constexpr int kBcrStamps = 32;
 #define BCR_STAMP(slot)                                                                          \
     do {                                                                                         \
         if ((d.diag & 8) && threadIdx.x == 0)                                                    \
-            d.bcr_stamps[(size_t)blockIdx.x * kBcrStamps + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+            d.bcr_stamps[(size_t)m * kBcrStamps + (slot)] = __builtin_amdgcn_s_memrealtime();         \
     } while (0)
 
 // tile index of Gram block (u, v), u >= v
@@ -155,32 +204,31 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
     TRIAL_GUARD
     if constexpr (BW >= 1 && BW <= kBcrMaxBW) {
         constexpr int NT = kBcrNT, S = 6 * BW, NB = 2 * BW + 1, RS = 6 * NB, WS = S + RS;
-        constexpr int TRI = bcr_tri(BW), NRT = BW * NB, NG = bcr_ngram(BW), XR = bcr_xrec(BW);
+        constexpr int TRI = bcr_tri(BW), NRT = BW * NB, NG = bcr_ngram(BW), NX = 2 * S + 1;
         constexpr size_t PUB = bcr_pub_doubles(BW);
         static_assert(TRI + NRT + NG <= NT, "one tile per thread");
         static_assert(S + RS <= NT, "one W column per thread");
-        constexpr int NPART = NT / S < kBcrParts ? NT / S : kBcrParts;  // mat-vec slices per row
         extern __shared__ __attribute__((aligned(16))) double lds[];
         double *Dm = lds, *Rm = Dm + S * S, *Wm = Rm + S * RS, *xv = Wm + S * WS;  // xv: x_a | x_c | x_m
         double *pv = xv + 3 * S;          // [2][48] pivot block factors: unit-lower L (36) + 1/d (6)
-        double *red = pv + 96;            // [kBcrParts][S]
-        double *ps = red + kBcrParts * S;  // [BW][24] Tcw | b_p | previous x_p of this row's poses, λ
         __shared__ uint32_t s_epoch;
-        __shared__ int s_fail;
-        __shared__ double s_sum[NT / 64];
-        __shared__ int s_kf[BW + 1];
-        const int tid = threadIdx.x, m = blockIdx.x, N = d.bcr_N, nf = d.nf;
+        __shared__ int s_fail, s_m;
+        const int tid = threadIdx.x, N = d.bcr_N, nf = d.nf;
         int L = 0;
         while ((1 << L) < N) ++L;
-        const bool root = m == 0;
-        const int lm = root ? L : __builtin_ctz(m);
-        const int a_row = root ? -1 : m - (1 << lm), c_row = root ? N : m + (1 << lm);
-        const bool hasU = !root, hasC = !root && c_row < N;
-        BCR_STAMP(0);
+        // super-row by ticket in level order (deadlock-free without co-residency, see the top)
         if (tid == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(&d.bcr_ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_m = bcr_row_fwd((int)t, N, L);
             s_epoch = __hip_atomic_load(&d.bcr_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
             s_fail = 0;
         }
+        __syncthreads();
+        const int m = s_m;
+        const bool root = m == 0;
+        const int lm = root ? L : __builtin_ctz(m);
+        const bool hasU = !root, hasC = !root && m + (1 << lm) < N;
+        BCR_STAMP(0);
         // ---- D_m (lower blocks; diagonal blocks full), b_m and, for odd m, the band couplings
         //      U = A(m, m-1), V = A(m, m+1); rows past nf are identity / zero. Every global load of
         //      a thread is issued before its LDS stores.
@@ -224,33 +272,6 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
                 if (tid + u * NT < S * RS) Rm[tid + u * NT] = vr[u];
         }
         for (int t = tid; t < S * WS; t += NT) Wm[t] = 0.0;
-        // this super-row's poses (updated at the very end): current Tcw, b_p, previous x_p, λ
-        // staged now, off the critical path; fixed poses k ≡ m (mod N) copied to the trial state
-        const int cur0 = d.ctrl->cur;
-        {
-            const double *Tc0 = d.Tb[cur0];
-            double *Tt0 = d.Tb[cur0 ^ 1];
-            if (tid < BW) s_kf[tid] = m * BW + tid < nf ? d.h_kf[m * BW + tid] : 0;
-            for (int t = tid; t < BW * 24; t += NT) {
-                const int i = t / 24, q = t % 24, h = m * BW + i;
-                double v = 0.0;
-                if (h < nf) {
-                    const int kf = d.h_kf[h];
-                    v = q < 12 ? Tc0[(size_t)kf * 12 + q] : (q < 18 ? d.bp[(size_t)h * 6 + q - 12] : d.xp[(size_t)h * 6 + q - 18]);
-                }
-                ps[t] = v;
-            }
-            if (tid == 0) ps[BW * 24] = d.ctrl->lambda;
-            const bool hlm0 = d.ctrl->hlm != 0;
-            for (int k = m + N * tid; k < d.n_kf; k += N * NT)
-                if (d.kf_hidx[k] < 0) {
-#pragma unroll
-                    for (int q = 0; q < 12; ++q) Tt0[(size_t)k * 12 + q] = Tc0[(size_t)k * 12 + q];
-                    if (hlm0)
-#pragma unroll
-                        for (int q = 0; q < 6; ++q) d.xk[cur0 ^ 1][(size_t)k * 6 + q] = d.xk[cur0][(size_t)k * 6 + q];
-                }
-        }
         __syncthreads();
         BCR_STAMP(1);
         // ---- survivor phases: contributions of the neighbours eliminated at levels < lm. Every
@@ -458,20 +479,100 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
             __syncthreads();
         }
         BCR_STAMP(14);
-        double *xa = xv, *xc = xv + S, *xm = xv + 2 * S;
-        double fail_tot = fail_fwd;  // root: everything has flowed in; others: from a (and c)
+        // ---- X = D_m⁻¹ [U | V | b] for the backward kernel; the root holds the solution x_0 itself
         if (!root) {
-            if (tid == 0 && !bcr_poll(&d.bcr_flag[2 * a_row + 1], epoch, &d.ctrl->dev_error, d.diag)) s_fail = 1;
-            if (hasC && tid == 64 && !bcr_poll(&d.bcr_flag[2 * c_row + 1], epoch, &d.ctrl->dev_error, d.diag)) s_fail = 1;
+            double *Xg = d.bcr_X + (size_t)m * S * NX;
+            for (int t = tid; t < S * NX; t += NT) Xg[t] = Rm[(t / NX) * RS + t % NX];
+        } else {
+            for (int r = tid; r < S; r += NT) st_sc1(d.bcr_x + r, Rm[r * RS + 2 * S]);
+            if (tid == 0) d.ctrl->solve_ok = fail_fwd != 0.0 ? 0 : 1;  // every failure word has flowed in
+            bcr_publish(&d.bcr_flag[1], epoch);
+        }
+        BCR_STAMP(16);
+        // ---- arrival: the last workgroup resets the ticket counter for the next launch
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t old = __hip_atomic_fetch_add(&d.bcr_ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == (uint32_t)(N - 1)) {
+                __hip_atomic_store(&d.bcr_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d.bcr_ctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        BCR_STAMP(17);
+    }
+}
+
+// Backward launch: x of every super-row from the root down, then the pose update (oplus into the
+// trial state, x_p kept from the previous trial when the solve failed — A13 — and the pose part of
+// Σx(λx+b) per row; fixed poses k ≡ m (mod N) copied to the trial state).
+template <int BW>
+__global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d) {
+    TRIAL_GUARD
+    if constexpr (BW >= 1 && BW <= kBcrMaxBW) {
+        constexpr int NT = kBcrBackNT, S = 6 * BW, NX = 2 * S + 1, XR = bcr_xrec(BW);
+        constexpr int NPART = NT / S < kBcrParts ? NT / S : kBcrParts;  // mat-vec slices per row
+        extern __shared__ __attribute__((aligned(16))) double lds[];
+        double *Xm = lds, *xa = Xm + bcr_X_doubles(BW), *xc = xa + S, *xm = xc + S, *red = xm + S;
+        double *ps = red + kBcrParts * S;  // [BW][24] Tcw | b_p | previous x_p of this row's poses, λ
+        __shared__ uint32_t s_epoch;
+        __shared__ int s_m;
+        __shared__ double s_sum[NT / 64];
+        __shared__ int s_kf[BW + 1];
+        const int tid = threadIdx.x, N = d.bcr_N, nf = d.nf;
+        int L = 0;
+        while ((1 << L) < N) ++L;
+        if (tid == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(&d.bcr_ctl[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_m = bcr_row_bwd((int)t, N, L);
+            s_epoch = __hip_atomic_load(&d.bcr_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        }
+        __syncthreads();
+        const int m = s_m;
+        const bool root = m == 0;
+        const int lm = root ? L : __builtin_ctz(m);
+        const int a_row = m - (1 << lm), c_row = m + (1 << lm);
+        const bool hasC = !root && c_row < N;
+        const uint32_t epoch = s_epoch;
+        // X_m into LDS and this row's poses (current Tcw, b_p, previous x_p, λ), issued before the waits
+        if (!root) {
+            const double *Xg = d.bcr_X + (size_t)m * S * NX;
+            for (int t = tid; t < S * NX; t += NT) Xm[t] = Xg[t];
+        }
+        const int cur0 = d.ctrl->cur;
+        const double *Tc0 = d.Tb[cur0];
+        double *Tt0 = d.Tb[cur0 ^ 1];
+        if (tid < BW) s_kf[tid] = m * BW + tid < nf ? d.h_kf[m * BW + tid] : 0;
+        for (int t = tid; t < BW * 24; t += NT) {
+            const int i = t / 24, q = t % 24, h = m * BW + i;
+            double v = 0.0;
+            if (h < nf) {
+                const int kf = d.h_kf[h];
+                v = q < 12 ? Tc0[(size_t)kf * 12 + q] : (q < 18 ? d.bp[(size_t)h * 6 + q - 12] : d.xp[(size_t)h * 6 + q - 18]);
+            }
+            ps[t] = v;
+        }
+        if (tid == 0) ps[BW * 24] = d.ctrl->lambda;
+        const bool hlm0 = d.ctrl->hlm != 0;
+        for (int k = m + N * tid; k < d.n_kf; k += N * NT)
+            if (d.kf_hidx[k] < 0) {
+#pragma unroll
+                for (int q = 0; q < 12; ++q) Tt0[(size_t)k * 12 + q] = Tc0[(size_t)k * 12 + q];
+                if (hlm0)
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) d.xk[cur0 ^ 1][(size_t)k * 6 + q] = d.xk[cur0][(size_t)k * 6 + q];
+            }
+        if (!root) {
+            // (a timeout raises Ctrl::dev_error: the host discards this schedule and re-solves)
+            if (tid == 0) (void)bcr_poll(&d.bcr_flag[2 * a_row + 1], epoch, &d.ctrl->dev_error, d.diag);
+            if (hasC && tid == 64) (void)bcr_poll(&d.bcr_flag[2 * c_row + 1], epoch, &d.ctrl->dev_error, d.diag);
             __syncthreads();
             for (int t = tid; t < S; t += NT) {
                 xa[t] = ld_sc1(d.bcr_x + (size_t)a_row * XR + t);
                 xc[t] = hasC ? ld_sc1(d.bcr_x + (size_t)c_row * XR + t) : 0.0;
             }
-            if (tid == 0) fail_tot = ld_sc1(d.bcr_x + (size_t)a_row * XR + S) + (s_fail ? 1.0 : 0.0);
             __syncthreads();
-            BCR_STAMP(15);
-            // mat-vec in kBcrParts column slices per row, partials summed in slice order
+            // mat-vec in column slices per row, partials summed in slice order
             if (tid < S * NPART) {
                 const int r = tid % S, part = tid / S;
                 constexpr int CPP = (2 * S + NPART - 1) / NPART;
@@ -479,30 +580,26 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
 #pragma unroll
                 for (int u = 0; u < CPP; ++u) {
                     const int q = part * CPP + u;
-                    if (q < S) sacc = fma(Rm[r * RS + q], xa[q], sacc);
-                    else if (q < 2 * S && hasC) sacc = fma(Rm[r * RS + q], xc[q - S], sacc);
+                    if (q < S) sacc = fma(Xm[r * NX + q], xa[q], sacc);
+                    else if (q < 2 * S && hasC) sacc = fma(Xm[r * NX + q], xc[q - S], sacc);
                 }
                 red[part * S + r] = sacc;
             }
             __syncthreads();
-        }
-        if (tid == 0) s_fail = fail_tot != 0.0 ? 1 : 0;
-        for (int r = tid; r < S; r += NT) {
-            double sacc = Rm[r * RS + 2 * S];
-            if (!root)
+            for (int r = tid; r < S; r += NT) {
+                double sacc = Xm[r * NX + 2 * S];
                 for (int part = 0; part < NPART; ++part) sacc -= red[part * S + r];
-            xm[r] = sacc;
-            st_sc1(d.bcr_x + (size_t)m * XR + r, sacc);
+                xm[r] = sacc;
+                st_sc1(d.bcr_x + (size_t)m * XR + r, sacc);
+            }
+            bcr_publish(&d.bcr_flag[2 * m + 1], epoch);
+        } else {
+            for (int r = tid; r < S; r += NT) xm[r] = d.bcr_x[r];  // solved by the forward root
+            __syncthreads();
         }
-        if (tid == 0) {
-            st_sc1(d.bcr_x + (size_t)m * XR + S, fail_tot);
-            if (root) d.ctrl->solve_ok = fail_tot != 0.0 ? 0 : 1;
-        }
-        bcr_publish(&d.bcr_flag[2 * m + 1], epoch);
-        BCR_STAMP(16);
         // ---- this super-row's poses: x_p (kept from the previous trial if the solve failed, A13),
         //      oplus into the trial state, pose part of Σx(λx+b)
-        const bool failed = s_fail != 0;
+        const bool failed = d.ctrl->solve_ok == 0;
         const double lam = ps[BW * 24];
         double sc = 0.0;
         if (tid < BW) {
@@ -532,14 +629,16 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
         }
         const double ssum = block_sum<NT>(sc, s_sum);
         if (tid == 0) d.part_ps[m] = ssum;
-        // ---- arrival: the last workgroup advances the epoch for the next launch
+        // ---- arrival: the last workgroup resets the tickets and advances the epoch
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         if (tid == 0) {
-            const uint32_t old = __hip_atomic_fetch_add(&d.bcr_ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t old = __hip_atomic_fetch_add(&d.bcr_ctl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (old == (uint32_t)(N - 1)) {
-                __hip_atomic_store(&d.bcr_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d.bcr_ctl[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d.bcr_ctl[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&d.bcr_ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        BCR_STAMP(17);
     }
 }

@@ -168,8 +168,9 @@ struct Dev {
     int32_t bcr, bcr_N;                 // enabled; super-rows (= workgroups of the launch)
     double *bcr_pub;                    // [N][bcr_pub_doubles(bw)] Schur contributions + coupling
     double *bcr_x;                      // [N][6 bw] solution of each super-row
+    double *bcr_X;                      // [N][6 bw][12 bw + 1] X = D_m⁻¹[U | V | b] (forward -> backward)
     uint32_t *bcr_flag;                 // [N][2] forward / backward hand-off flags (epoch)
-    uint32_t *bcr_ctl;                  // [4] epoch, arrival counter, failure, spare
+    uint32_t *bcr_ctl;                  // [kBcrCtl] epoch, forward arrivals / tickets, backward arrivals / tickets
     unsigned long long *bcr_stamps;     // [N][32] phase timestamps (PLBA_DIAG bit 8 only)
 };
 
@@ -272,17 +273,19 @@ __device__ __forceinline__ void lds_barrier() {
 // ---------------------------------------------------------------- linearisation
 // iteration kernels run for a new outer iteration and for the first one of a stage (the stage
 // switch — SparseOptimizer::initializeOptimization — is folded into them)
-#define ITER_GUARD                                                           \
-    {                                                                        \
-        const Ctrl *cg = d.ctrl;                                             \
-        if (cg->all_done || !(cg->need_iter || cg->switch_pending)) return;  \
+// (a bounded in-kernel wait that timed out — Ctrl::dev_error — stops every later kernel of the
+// batch; the host then re-solves the window with another factorisation)
+#define ITER_GUARD                                                                             \
+    {                                                                                          \
+        const Ctrl *cg = d.ctrl;                                                               \
+        if (cg->all_done || cg->dev_error || !(cg->need_iter || cg->switch_pending)) return;   \
     }
 constexpr double kChi2Thr = 5.991;  // src/mapHandler.cpp:6129,6142
 // a stage skipped by k_iter_init (no active edge) leaves switch_pending set: no trial
-#define TRIAL_GUARD                                          \
-    {                                                        \
-        const Ctrl *cg = d.ctrl;                             \
-        if (cg->all_done || cg->switch_pending) return;      \
+#define TRIAL_GUARD                                                          \
+    {                                                                        \
+        const Ctrl *cg = d.ctrl;                                             \
+        if (cg->all_done || cg->switch_pending || cg->dev_error) return;     \
     }
 
 __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {

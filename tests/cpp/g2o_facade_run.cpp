@@ -4,9 +4,13 @@
 // names, solved on the GPU through libplba.so. Eigen is not in this image, so Mat4/Vec/IsoInfo below
 // stand in for Eigen::Matrix4d / Vector2d,3d,4d / Matrix2d::Identity()*s (same element access).
 //
-// usage: g2o_facade_run <graph.bin> <out.bin>   (formats: tests/test_g2o_facade.py)
+// usage: g2o_facade_run <graph.bin> <out.bin> [mutate]   (formats: tests/test_g2o_facade.py)
+//   mutate: between the two optimize() calls, fix the first free keyframe, move the measurement of
+//           point edge 0 and scale the information of point edge 1 (g2o applies such changes at the
+//           next optimize(); the facade must re-marshal the window)
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "plba_g2o.hpp"
@@ -20,6 +24,20 @@ struct Vec {
     double a[4] = {};
     double &operator()(int i) { return a[i]; }
     double operator()(int i) const { return a[i]; }
+};
+// stand-ins for the map objects the read-back writes (KeyFrame::T_kf_w Matrix4d, MapPoint::point3D
+// Vector3d, MapLine NDw from Vector4d orth): the same member calls as src/mapHandler.cpp:6296-6319
+struct KeyFrame {
+    int kf_idx;
+    Mat4 T_kf_w;
+};
+struct MapPoint {
+    int idx;
+    Vec point3D;
+};
+struct MapLine {
+    int idx;
+    Vec orth_written;
 };
 struct IsoInfo {  // Eigen::Matrix<N,N>::Identity() * s
     double s;
@@ -127,8 +145,23 @@ int main(int argc, char **argv) {
         vlEdgesMono.push_back(ed);
     }
 
+    const bool mutate = argc > 3 && std::string(argv[3]) == "mutate";
     optimizer.initializeOptimization();
     const int it1 = optimizer.optimize(5);
+    if (mutate) {
+        for (int k = 0; k < nk; ++k)
+            if (!kffix[k]) {
+                optimizer.vertex(kfid[k])->setFixed(true);
+                break;
+            }
+        if (ne > 0) {
+            Vec obs;
+            obs(0) = eobs[0] + 3.0;
+            obs(1) = eobs[1] - 2.0;
+            vpEdgesMono[0]->setMeasurement(obs);
+        }
+        if (ne > 1) vpEdgesMono[1]->setInformation(IsoInfo{4.0 * einfo[1]});
+    }
     for (auto *e : vpEdgesMono) {
         if (e->chi2() > 5.991 || !e->isDepthPositive()) e->setLevel(1);
         e->setRobustKernel(0);
@@ -168,6 +201,31 @@ int main(int argc, char **argv) {
         const Mat4 T = static_cast<VertexLMPose *>(optimizer.vertex(kfid[k]))->estimate();
         for (int r = 0; r < 3; ++r) fwrite(&T.a[r * 4], sizeof(double), 4, o);
     }
+    // the reference's read-back statements, verbatim apart from the stand-in containers
+    // (src/mapHandler.cpp:6297-6319)
+    std::vector<KeyFrame> kfs(nk);
+    std::vector<MapPoint> local_pt(np);
+    std::vector<MapLine> local_ls(nl);
+    for (int k = 0; k < nk; ++k) kfs[k].kf_idx = kfid[k];
+    for (int p = 0; p < np; ++p) local_pt[p].idx = p;
+    for (int l = 0; l < nl; ++l) local_ls[l].idx = l;
+    for (int k = 0; k < nk; ++k) {
+        if (kffix[k]) continue;  // idx_nofix_kfs
+        KeyFrame *pKFi = &kfs[k];
+        VertexLMPose *vPose = dynamic_cast<VertexLMPose *>(optimizer.vertex(pKFi->kf_idx));
+        pKFi->T_kf_w = vPose->estimate().inverse();
+    }
+    for (MapPoint &mp : local_pt) {
+        MapPoint *pMP = &mp;
+        VertexLMPointXYZ *vPoint = dynamic_cast<VertexLMPointXYZ *>(optimizer.vertex(ptid[pMP->idx]));
+        pMP->point3D = vPoint->estimate();
+    }
+    for (MapLine &ml : local_ls) {
+        MapLine *lML = &ml;
+        VertexLMLineOrth *vLine = dynamic_cast<VertexLMLineOrth *>(optimizer.vertex(lnid[lML->idx]));
+        Vec orth = vLine->estimate();
+        lML->orth_written = orth;
+    }
     for (int p = 0; p < np; ++p) {
         const Vec x = static_cast<VertexLMPointXYZ *>(optimizer.vertex(ptid[p]))->estimate();
         fwrite(x.a, sizeof(double), 3, o);
@@ -181,6 +239,9 @@ int main(int argc, char **argv) {
     fwrite(plev.data(), 1, ne, o);
     fwrite(lchi.data(), sizeof(double), nle, o);
     fwrite(llev.data(), 1, nle, o);
+    for (int k = 0; k < nk; ++k) fwrite(kfs[k].T_kf_w.a, sizeof(double), 16, o);  // zero for fixed KFs
+    for (int p = 0; p < np; ++p) fwrite(local_pt[p].point3D.a, sizeof(double), 3, o);
+    for (int l = 0; l < nl; ++l) fwrite(local_ls[l].orth_written.a, sizeof(double), 4, o);
     fclose(o);
     return 0;
 }

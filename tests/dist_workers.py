@@ -97,7 +97,8 @@ def sharded_gpu_worker(rank, world, port, outdir, cfg, transport):
              **{k: v for k, v in out.items() if k not in ("trace", "solve_ms")},
              trace_chi2=np.array([t["chi2_end"] for t in out["trace"]]),
              rerun_equal=np.array(all(np.array_equal(out[k], out2[k]) for k in ("kf_Tcw", "pt_xyz", "ln_orth"))),
-             local_landmarks=np.array(st["landmarks"]), local_edges=np.array(st["edges"]))
+             local_landmarks=np.array(st["landmarks"]), local_edges=np.array(st["edges"]),
+             bcr_fallbacks=np.array(st["bcr_fallbacks"]))
     s.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -1,8 +1,16 @@
 """Parity helpers shared by the GPU tests (oracle vs HIP path)."""
+import json
+import os
+
 import numpy as np
 
-# north_star: final pose/landmark estimates within 1e-4 relative of the reference path.
+# north_star: final pose/landmark estimates within 1e-4 relative of the reference path (reported
+# metric, `row_rel_err`). The asserted bar is much tighter: element-wise relative
+# 1e-8 where |ref| > 1e-3, absolute 1e-10 elsewhere (observed agreement: 1e-11 .. 1e-15).
 EST_RTOL = 1e-4
+ELEM_RTOL = 1e-8
+ELEM_ATOL = 1e-10
+ELEM_BIG = 1e-3
 
 
 def rel_err(a, b):
@@ -25,12 +33,38 @@ def row_rel_err(a, b):
     return float((num / den).max())
 
 
+def elem_violation(a, b, rtol=ELEM_RTOL, atol=ELEM_ATOL, big=ELEM_BIG):
+    """max over elements of |a-b| / (rtol |b|) where |b| > big, |a-b| / atol elsewhere: <= 1 passes."""
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    if b.size == 0:
+        return 0.0
+    d = np.abs(a - b)
+    scale = np.where(np.abs(b) > big, rtol * np.abs(b), atol)
+    return float((d / scale).max())
+
+
+def assert_parity(m, elem=1.0, north=EST_RTOL):
+    """Both bars: the north_star 1e-4 row-relative metric and the element-wise tight bar."""
+    log = os.environ.get("PLBA_PARITY_LOG")
+    if log:  # diagnostics: every checked metric, one JSON line per check
+        with open(log, "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "?"), "elem_bar": elem,
+                                **{k: (float(v) if not isinstance(v, list) else [float(x) for x in v])
+                                   for k, v in m.items()}}) + "\n")
+    assert m["Tcw"] < north and m["pt"] < north and m["ln"] < north, m
+    assert m["Tcw_elem"] <= elem and m["pt_elem"] <= elem and m["ln_elem"] <= elem, m
+
+
 def compare(gpu: dict, ref: dict, rtol=EST_RTOL):
     """Returns a dict of error metrics; asserts nothing."""
     return dict(
         Tcw=row_rel_err(gpu["kf_Tcw"], ref["kf_Tcw"]),
         pt=row_rel_err(gpu["pt_xyz"], ref["pt_xyz"]),
         ln=row_rel_err(gpu["ln_orth"], ref["ln_orth"]),
+        Tcw_elem=elem_violation(gpu["kf_Tcw"], ref["kf_Tcw"]),
+        pt_elem=elem_violation(gpu["pt_xyz"], ref["pt_xyz"]),
+        ln_elem=elem_violation(gpu["ln_orth"], ref["ln_orth"]),
         chi2_stage=[abs(gpu["chi2"][i] - ref["chi2"][i]) / max(abs(ref["chi2"][i]), 1e-300) for i in range(2)],
         pt_level_diff=int((gpu["ept_level"] != ref["ept_level"]).sum()),
         ln_level_diff=int((gpu["eln_level"] != ref["eln_level"]).sum()),

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle_api as oa
-from parity import EST_RTOL, compare
+from parity import EST_RTOL, assert_parity, compare
 from plba import synth
 
 pytestmark = pytest.mark.gpu
@@ -26,7 +26,7 @@ def solver():
 def _check(out, ref):
     m = compare(out, ref)
     assert m["pt_level_diff"] == 0 and m["ln_level_diff"] == 0, m
-    assert m["Tcw"] < EST_RTOL and m["pt"] < EST_RTOL and m["ln"] < EST_RTOL, m
+    assert_parity(m)
     np.testing.assert_array_equal(out["iters"], ref["iters"])
     return m
 

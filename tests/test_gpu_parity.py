@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle_api as oa
-from parity import EST_RTOL, compare
+from parity import EST_RTOL, assert_parity, compare
 from plba import synth
 
 pytestmark = pytest.mark.gpu
@@ -29,7 +29,7 @@ def test_lba_matches_oracle(solver, cfg):
     out = solver.lba_plucker()
     m = compare(out, ref)
     assert m["pt_level_diff"] == 0 and m["ln_level_diff"] == 0, m
-    assert m["Tcw"] < EST_RTOL and m["pt"] < EST_RTOL and m["ln"] < EST_RTOL, m
+    assert_parity(m)
     assert max(m["chi2_stage"]) < 1e-6, m
     # both optimize() calls run the same number of outer iterations
     np.testing.assert_array_equal(out["iters"], ref["iters"])
