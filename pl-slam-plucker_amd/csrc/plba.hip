@@ -100,6 +100,8 @@ struct plba_ctx {
     // captured step graph (one LM trial + guarded iteration / stage-switch work)
     hipGraph_t step_graph = nullptr;
     hipGraphExec_t step_exec = nullptr;
+    bool graphs_stale = false;  // captured for a previous window (update before use)
+    std::vector<int64_t> graph_sig;  // launch signature the executable graphs were built for
     // the same step captured 2, 4, 8, 16 times back to back: a batch of N steps is launched as
     // its binary decomposition (a graph-to-graph transition costs ~8 us on the device)
     static constexpr int kMultiLevels = 4;
@@ -140,17 +142,11 @@ struct plba_ctx {
         err = buf;
         if (opts.verbose) fprintf(stderr, "[plba] %s\n", buf);
     }
+    // A new window keeps the instantiated step graphs: the next capture updates them in place
+    // (hipGraphExecUpdate, same topology, new kernel arguments and grids) instead of destroying
+    // and re-instantiating five executable graphs (capture_step).
     void free_all() {
-        if (step_exec) (void)hipGraphExecDestroy(step_exec);
-        if (step_graph) (void)hipGraphDestroy(step_graph);
-        step_exec = nullptr;
-        step_graph = nullptr;
-        for (int i = 0; i < kMultiLevels; ++i) {
-            if (multi_exec[i]) (void)hipGraphExecDestroy(multi_exec[i]);
-            if (multi_graph[i]) (void)hipGraphDestroy(multi_graph[i]);
-            multi_exec[i] = nullptr;
-            multi_graph[i] = nullptr;
-        }
+        graphs_stale = true;
         plan.clear();
         d = Dev{};
         bk_T = bk_X = bk_xp = bk_xk = bk_Lpb = bk_XL = bk_xl = nullptr;
@@ -1229,6 +1225,19 @@ int launch_step(plba_ctx *ctx) {
     return PLBA_OK;
 }
 
+void destroy_graphs(plba_ctx *ctx) {
+    if (ctx->step_exec) (void)hipGraphExecDestroy(ctx->step_exec);
+    if (ctx->step_graph) (void)hipGraphDestroy(ctx->step_graph);
+    ctx->step_exec = nullptr;
+    ctx->step_graph = nullptr;
+    for (int i = 0; i < plba_ctx::kMultiLevels; ++i) {
+        if (ctx->multi_exec[i]) (void)hipGraphExecDestroy(ctx->multi_exec[i]);
+        if (ctx->multi_graph[i]) (void)hipGraphDestroy(ctx->multi_graph[i]);
+        ctx->multi_exec[i] = nullptr;
+        ctx->multi_graph[i] = nullptr;
+    }
+}
+
 int capture_steps(plba_ctx *ctx, int nsteps, hipGraph_t &graph, hipGraphExec_t &exec) {
     const bool t = ctx->timing;
     ctx->timing = false;
@@ -1246,12 +1255,38 @@ int capture_steps(plba_ctx *ctx, int nsteps, hipGraph_t &graph, hipGraphExec_t &
         ctx->set_error("graph capture failed: %s", hipGetErrorString(e));
         return PLBA_E_DEVICE;
     }
+    if (exec) {  // a previous window's executable graph: update it in place when the topology matches
+        hipGraphNode_t bad = nullptr;
+        hipGraphExecUpdateResult res = hipGraphExecUpdateSuccess;
+        if (hipGraphExecUpdate(exec, g, &bad, &res) == hipSuccess && res == hipGraphExecUpdateSuccess) {
+            if (graph) (void)hipGraphDestroy(graph);
+            graph = g;
+            return PLBA_OK;
+        }
+        (void)hipGetLastError();
+        (void)hipGraphExecDestroy(exec);
+        exec = nullptr;
+    }
+    if (graph) (void)hipGraphDestroy(graph);
     graph = g;
     PLBA_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
     return PLBA_OK;
 }
+// Which kernels (template instances) a step launches, in which order: an executable graph is
+// updated in place only for a window with the same signature (hipGraphExecUpdate changes kernel
+// arguments and grids, never the kernel a node runs).
+std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
+    const Dev &d = ctx->d;
+    return {d.E > 0, d.nf > 0, d.n_lm > 0, d.n > 0, d.nch > 0, d.band_mode, d.dense_mfma, d.dense_mfma ? d.ntiles : 0,
+            d.bw, d.bcr, d.cl, d.twisted, d.sharded, d.fold, d.fold_init, d.n_kf > 0,
+            (int64_t)(getenv("PLBA_CHUNK_DIRECT") != nullptr), (int64_t)ctx->comm.kind};
+}
 int capture_step(plba_ctx *ctx) {
-    if (ctx->step_exec) return PLBA_OK;
+    if (ctx->step_exec && !ctx->graphs_stale) return PLBA_OK;
+    ctx->graphs_stale = false;
+    const std::vector<int64_t> sig = launch_signature(ctx);
+    if (ctx->step_exec && sig != ctx->graph_sig) destroy_graphs(ctx);  // different kernels: rebuild
+    ctx->graph_sig = sig;
     const auto t0 = std::chrono::steady_clock::now();
     int rc = capture_steps(ctx, 1, ctx->step_graph, ctx->step_exec);
     for (int i = 0; i < plba_ctx::kMultiLevels && !rc; ++i)
@@ -1280,18 +1315,6 @@ int read_ctrl(plba_ctx *ctx) {
     return PLBA_OK;
 }
 
-void destroy_graphs(plba_ctx *ctx) {
-    if (ctx->step_exec) (void)hipGraphExecDestroy(ctx->step_exec);
-    if (ctx->step_graph) (void)hipGraphDestroy(ctx->step_graph);
-    ctx->step_exec = nullptr;
-    ctx->step_graph = nullptr;
-    for (int i = 0; i < plba_ctx::kMultiLevels; ++i) {
-        if (ctx->multi_exec[i]) (void)hipGraphExecDestroy(ctx->multi_exec[i]);
-        if (ctx->multi_graph[i]) (void)hipGraphDestroy(ctx->multi_graph[i]);
-        ctx->multi_exec[i] = nullptr;
-        ctx->multi_graph[i] = nullptr;
-    }
-}
 
 // Copies of the state a schedule starts from (BCR windows only): save = true before the first
 // batch, save = false to put it back after a hand-off timeout.
@@ -1526,6 +1549,7 @@ int plba_destroy(plba_ctx *ctx) {
     (void)hipSetDevice(ctx->opts.device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->free_all();
+    destroy_graphs(ctx);
     if (ctx->arena) (void)hipFree(ctx->arena);
     if (ctx->staging) (void)hipHostFree(ctx->staging);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);

@@ -906,19 +906,39 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
                 w2[j] = reinterpret_cast<const dbl2 *>(d.Z + (size_t)f2 * 8)[k];
             }
             __syncthreads();  // the previous batch's rows are read (one wave: a cheap barrier)
+            // Bank-conflict-free row reads (ds_read_b128: 16-lane groups, bank (a/4) mod 64):
+            //  Z rows (4 pieces, 64-B stride: lanes l, l+4, l+8, l+12 share a bank window) are
+            //  stored rotated by ρ(r) = (r >> 2) & 3 pieces, so the lane reading its row at step k
+            //  fetches piece k from position (k + ρ) mod 4; stores stay conflict-free.
+            //  A rows (6 pieces, 96-B stride: lanes l and l+8 collide) are stored linearly and read
+            //  rotated by ρ = (lane >> 3) & 1, the pieces put back in order with selects (rotating
+            //  the stores instead would move the conflicts to the stores).
 #pragma unroll
             for (int j = 0; j < 6; ++j) { sA1[64 * j + lane] = v1[j]; sA2[64 * j + lane] = v2[j]; }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { sZ1[64 * j + lane] = w1[j]; sZ2[64 * j + lane] = w2[j]; }
+            for (int j = 0; j < 4; ++j) {
+                const int r = 16 * j + (lane >> 2), k = lane & 3, pos = 4 * r + ((k + ((r >> 2) & 3)) & 3);
+                sZ1[pos] = w1[j];
+                sZ2[pos] = w2[j];
+            }
             __syncthreads();
+            const int ra = (lane >> 3) & 1, rz = (lane >> 2) & 3;
+            dbl2 tA1[6], tA2[6];
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
-                const dbl2 x = sA1[6 * lane + k], y = sA2[6 * lane + k];
+                const int pk = k + ra < 6 ? k + ra : k + ra - 6;
+                tA1[k] = sA1[6 * lane + pk];
+                tA2[k] = sA2[6 * lane + pk];
+            }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {  // piece k sits in tA[k] (ra = 0) or tA[k - 1] (ra = 1)
+                const dbl2 x = ra ? tA1[(k + 5) % 6] : tA1[k], y = ra ? tA2[(k + 5) % 6] : tA2[k];
                 a1[2 * k] = x.x; a1[2 * k + 1] = x.y; a2[2 * k] = y.x; a2[2 * k + 1] = y.y;
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const dbl2 x = sZ1[4 * lane + k], y = sZ2[4 * lane + k];
+                const int pos = 4 * lane + ((k + rz) & 3);
+                const dbl2 x = sZ1[pos], y = sZ2[pos];
                 z1[2 * k] = x.x; z1[2 * k + 1] = x.y; z2[2 * k] = y.x; z2[2 * k + 1] = y.y;
             }
         } else {

@@ -98,3 +98,22 @@ def test_device_build_reuses_context_across_sizes(monkeypatch):
         _, fresh = _solve(monkeypatch, g, host=False)
         for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_level"):
             assert np.array_equal(o[k], fresh[k]), k
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+def test_step_graph_update_across_windows(monkeypatch, cfg):
+    """Consecutive windows with the same launch signature (C2: column-lane, C4: BCR) reuse the
+    executable step graphs through hipGraphExecUpdate: each solve equals a fresh context's."""
+    from plba.lib import Solver
+    seeds = [synth.CONFIGS[cfg][3] + 101 * k for k in range(3)]
+    gs = [synth.generate(cfg, seed=sd) for sd in seeds]
+    with Solver() as s:
+        outs = []
+        for g in gs:
+            s.upload(g)
+            outs.append(s.lba_plucker())
+            assert s.structure_stats()["graph"] == 1
+    for g, o in zip(gs, outs):
+        _, fresh = _solve(monkeypatch, g, host=False)
+        for k in KEYS:
+            assert np.array_equal(o[k], fresh[k]), k
