@@ -212,7 +212,10 @@ void plba_hlm_default_params(plba_hlm_params *p);
 /* The whole loop on the uploaded window, on the device (one captured step per iteration).
  * Per-iteration records (plba_get_trace): stage 0, iter, trials 1, result 0 = DX applied,
  * 1 = DX rejected (err > err_prev), 3 = stopped before the solve; chi2_start = chi2_end = err,
- * lambda_start / lambda_end around the iteration. */
+ * lambda_start / lambda_end around the iteration.
+ * Deliberate divergence (INTEGRATION.md B'): a free keyframe with no active observation gets 1.0
+ * on its diagonal (DX = 0) and a zero pivot elsewhere keeps X unchanged, where the reference's
+ * Eigen SimplicialLDLT would solve on a partial factor and produce inf / NaN. */
 int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params *p, plba_hlm_result *res);
 
 /* ---- Loop-closure pose graph:

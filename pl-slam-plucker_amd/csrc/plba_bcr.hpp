@@ -89,9 +89,33 @@ __host__ __device__ constexpr size_t bcr_lds_doubles(int bw) {
            (size_t)(6 * bw) * (6 * bw + 6 * (2 * bw + 1)) + 3 * (size_t)(6 * bw) + 96 + (size_t)kBcrParts * (6 * bw) +
            (size_t)bw * 24 + 2;
 }
-// published record of an eliminated super-row, element-major for coalesced write-through
-// stores: [36][ngram] Gram tiles (F = A(c,a) tiles stored negated) + 1 failure word
-__host__ __device__ constexpr size_t bcr_pub_doubles(int bw) { return (size_t)36 * bcr_ngram(bw) + 2; }
+// published record of an eliminated super-row: its Gram matrix G = Rᵀ D_m⁻¹ R over [U | V | b]
+// (RS = 6(2bw+1) columns, b padded to 6) as a grid of 16x16 tiles, each tile row-major (the
+// MFMA accumulator layout), only tiles (I, J) with J <= I + 1 written; + 1 failure word
+#define BCR_T16(bw) ((6 * (2 * (bw) + 1) + 15) / 16)
+__host__ __device__ constexpr size_t bcr_pub_doubles(int bw) { return (size_t)BCR_T16(bw) * BCR_T16(bw) * 256 + 2; }
+// index of G(p, q) in a record
+__host__ __device__ constexpr size_t bcr_gidx(int bw, int p, int q) {
+    return ((size_t)(p / 16) * BCR_T16(bw) + q / 16) * 256 + (p % 16) * 16 + q % 16;
+}
+// the written tiles: row I, columns J = 0 .. min(I + 1, T16 - 1)
+__host__ __device__ constexpr int bcr_gram_tiles(int bw) {
+    int n = 0;
+    for (int I = 0; I < BCR_T16(bw); ++I) n += (I + 1 < BCR_T16(bw) ? I + 1 : BCR_T16(bw) - 1) + 1;
+    return n;
+}
+__host__ __device__ inline void bcr_gram_tile(int bw, int t, int &I, int &J) {
+    const int T = BCR_T16(bw);
+    for (I = 0; I < T; ++I) {
+        const int cnt = (I + 1 < T ? I + 1 : T - 1) + 1;
+        if (t < cnt) {
+            J = t;
+            return;
+        }
+        t -= cnt;
+    }
+    I = J = 0;
+}
 // solution record of a super-row: x (6 bw), padded
 __host__ __device__ constexpr int bcr_xrec(int bw) { return 6 * bw + 2; }
 // X = D_m⁻¹ [U | V | b] of an eliminated super-row, [6 bw][12 bw + 1] row-major
@@ -288,32 +312,33 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
             const bool fU = takeF && ha && !root, fV = takeF && hb && hasC;
             constexpr int KD = (TRI * 36 + NT - 1) / NT, KF = (S * S + NT - 1) / NT;
             double gda[KD], gdb[KD], gfa[KF], gfb[KF], gba = 0.0, gbb = 0.0, fa = 0.0, fb = 0.0;
-            // D_m -= G_VV(above) + G_UU(below)   (lower blocks, element-major records)
+            // D_m -= G_VV(above) + G_UU(below)   (lower blocks; G entries from the 16x16-tile records)
 #pragma unroll
             for (int u = 0; u < KD; ++u) {
                 const int t = tid + u * NT, blk = t % TRI, e = t / TRI;
                 int bi, bj;
                 tri_decode(blk, bi, bj);
                 const bool ok = t < TRI * 36;
-                gda[u] = ok && ha ? ld_sc1(pa + (size_t)e * NG + gtile(BW + bi, BW + bj)) : 0.0;
-                gdb[u] = ok && hb ? ld_sc1(pb + (size_t)e * NG + gtile(bi, bj)) : 0.0;
+                const int r = 6 * bi + e / 6, c = 6 * bj + e % 6;
+                gda[u] = ok && ha ? ld_sc1(pa + bcr_gidx(BW, S + r, S + c)) : 0.0;
+                gdb[u] = ok && hb ? ld_sc1(pb + bcr_gidx(BW, r, c)) : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < KF; ++u) {
                 const int t = tid + u * NT, blk = t % (BW * BW), e = t / (BW * BW), vb = blk / BW, ub = blk % BW;
                 const bool ok = t < S * S;
-                const size_t o = (size_t)e * NG + gtile(BW + vb, ub);  // F = A(c_n, a_n) (stored negated)
-                gfa[u] = ok && fU ? ld_sc1(pa + o) : 0.0;
-                gfb[u] = ok && fV ? ld_sc1(pb + o) : 0.0;
+                const size_t o = bcr_gidx(BW, S + 6 * vb + e / 6, 6 * ub + e % 6);  // F = A(c_n, a_n) = -G_VU
+                gfa[u] = ok && fU ? -ld_sc1(pa + o) : 0.0;
+                gfb[u] = ok && fV ? -ld_sc1(pb + o) : 0.0;
             }
-            if (tid < S) {  // b_m -= g_Vb(above) + g_Ub(below): row 0 of the b-row tiles
-                const int vb = tid / 6, e = tid % 6;
-                gba = ha ? ld_sc1(pa + (size_t)e * NG + gtile(2 * BW, BW + vb)) : 0.0;
-                gbb = hb ? ld_sc1(pb + (size_t)e * NG + gtile(2 * BW, vb)) : 0.0;
+            if (tid < S) {  // b_m -= g_Vb(above) + g_Ub(below)
+                gba = ha ? ld_sc1(pa + bcr_gidx(BW, 2 * S, S + tid)) : 0.0;
+                gbb = hb ? ld_sc1(pb + bcr_gidx(BW, 2 * S, tid)) : 0.0;
             }
             if (tid == 0) {
-                fa = ha ? ld_sc1(pa + (size_t)36 * NG) : 0.0;
-                fb = hb ? ld_sc1(pb + (size_t)36 * NG) : 0.0;
+                constexpr size_t FW = (size_t)BCR_T16(BW) * BCR_T16(BW) * 256;
+                fa = ha ? ld_sc1(pa + FW) : 0.0;
+                fb = hb ? ld_sc1(pb + FW) : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < KD; ++u) {
@@ -338,31 +363,12 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
             __syncthreads();
             BCR_STAMP(2 + lp);
         }
-        // ---- elimination of super-row m. One 6x6 tile per thread, kept in registers:
-        //      D tiles (i >= j), RHS tiles (i, column block), Gram tiles (u >= v); every tile does
-        //      acc += A·B per step with A = -D(i,k) (D, RHS) or R'(k,u)ᵀ (Gram), B = W(k, ·).
-        auto rhs_on = [&](int bc) { return bc == 2 * BW || (bc < BW ? hasU : hasC); };
-        int role = 0, ti = 0, tj = 0;
-        if (tid < TRI) {
-            role = 1;
-            tri_decode(tid, ti, tj);
-        } else if (tid < TRI + NRT) {
-            role = 2;
-            ti = (tid - TRI) / NB;
-            tj = (tid - TRI) % NB;
-            if (!rhs_on(tj)) role = 0;
-        } else if (tid < TRI + NRT + NG) {
-            role = 3;
-            tri_decode(tid - TRI - NRT, ti, tj);
-            if (root || !rhs_on(ti) || !rhs_on(tj)) role = 0;
-        }
-        double acc[36];
-        if (role == 1) lds_tile(Dm + (6 * ti) * S + 6 * tj, S, acc);
-        else if (role == 2) lds_tile(Rm + (6 * ti) * RS + 6 * tj, RS, acc);
-        else {
-#pragma unroll
-            for (int e = 0; e < 36; ++e) acc[e] = 0.0;
-        }
+        // ---- elimination of super-row m: block LDLᵀ of D_m with 6x6 pivots, [U | V | b] carried
+        //      as right-hand sides. Step k: W(k, ·) = P_k⁻¹ M(k, ·) (one thread per column), then
+        //      the trailing update of D and R in LDS as half-tile tasks (3 rows x 6 columns, K = 6)
+        //      spread over waves 0-6, while wave 7 updates the next pivot block first and factors it
+        //      (lookahead). Rows of R are final once their block is the pivot (R'), so the Gram
+        //      G = R'ᵀ W_R = Rᵀ D_m⁻¹ R is one rank-S product at the end, on the matrix cores.
         bool fail = false;
         auto factor_pivot = [&](const double (&p)[36], double *dst) {
             double l[36], dinv[6];
@@ -374,13 +380,19 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
 #pragma unroll
             for (int e = 0; e < 6; ++e) dst[36 + e] = dinv[e];
         };
-        if (tid == 0) factor_pivot(acc, pv);  // tile (0,0) = P_0
+        if (tid == 0) {
+            double p0[36];
+            lds_tile(Dm, S, p0);
+            factor_pivot(p0, pv);  // P_0
+        }
         __syncthreads();
         const int nU = hasU ? S : 0, nV = hasC ? S : 0;
+        const int nRB = (hasU ? BW : 0) + (hasC ? BW : 0) + 1;  // active R column blocks
+        constexpr int NTW = NT - 64;                             // task threads (waves 0-6)
         for (int k = 0; k < BW; ++k) {
             const double *pk = pv + 48 * (k & 1);
-            // phase 1: W(k, col) = P_k⁻¹ M(k, col) for the D columns of later blocks and the
-            // active RHS columns (P_k factors broadcast from LDS)
+            // A2: W(k, col) = P_k⁻¹ M(k, col) for the D columns of later blocks and the active R
+            // columns (P_k factors broadcast from LDS)
             const int nWd = S - 6 * (k + 1);
             if (tid < nWd + nU + nV + 1 && !(d.diag & 32)) {  // (diag 32/16: timing experiments only)
                 double v[6];
@@ -407,35 +419,96 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
                 for (int q = 0; q < 6; ++q) Wm[(6 * k + q) * WS + col] = v[q];
             }
             __syncthreads();
-            // phase 2
-            const bool act = (role == 1 && tj > k) || (role == 2 && ti > k) || role == 3;
-            if (act && !(d.diag & 16)) {
-                double at[36], bt[36];
-                if (role == 3) {
-                    double rt[36];
-                    lds_tile(Rm + (6 * k) * RS + 6 * ti, RS, rt);
+            if (k + 1 < BW && !(d.diag & 16)) {
+                const double *Wk = Wm + (size_t)(6 * k) * WS;
+                if (tid >= NTW) {
+                    // lookahead: the next pivot block P_{k+1} = D(k+1,k+1) - D(k+1,k) W(k,k+1), one
+                    // entry per lane, then factored by one lane
+                    const int lane = tid - NTW;
+                    if (lane < 36) {
+                        const int r = 6 * (k + 1) + lane / 6, c = 6 * (k + 1) + lane % 6;
+                        double sacc = Dm[r * S + c];
 #pragma unroll
-                    for (int q = 0; q < 6; ++q)
-#pragma unroll
-                        for (int ea = 0; ea < 6; ++ea) at[ea * 6 + q] = rt[q * 6 + ea];
+                        for (int q = 0; q < 6; ++q) sacc = fma(-Dm[r * S + 6 * k + q], Wk[q * WS + c], sacc);
+                        Dm[r * S + c] = sacc;
+                    }
+                    wave_lds_sync();
+                    if (lane == 0) {
+                        double p1[36];
+                        lds_tile(Dm + (6 * (k + 1)) * S + 6 * (k + 1), S, p1);
+                        factor_pivot(p1, pv + 48 * ((k + 1) & 1));
+                    }
                 } else {
-                    lds_tile(Dm + (6 * ti) * S + 6 * k, S, at);
+                    // A3: half-tile tasks (block row bi > k, rows 6bi + 3h .. + 2, column block cb):
+                    // D blocks k < cb <= bi except the pivot block (k+1, k+1), then the R blocks
+                    int nD = 0;
+                    for (int bi = k + 1; bi < BW; ++bi) nD += bi - k;
+                    nD = 2 * (nD - 1);
+                    const int nTask = nD + 2 * (BW - 1 - k) * nRB;
+                    for (int t = tid; t < nTask; t += NTW) {
+                        int bi, cb, h;
+                        bool isD = t < nD;
+                        if (isD) {
+                            int r = t / 2 + 1;  // skip the pivot block, the first D block in this order
+                            h = t & 1;
+                            bi = k + 1;
+                            while (r >= bi - k) {
+                                r -= bi - k;
+                                ++bi;
+                            }
+                            cb = k + 1 + r;
+                        } else {
+                            const int t2 = t - nD;
+                            h = t2 & 1;
+                            const int rest = t2 >> 1;
+                            bi = k + 1 + rest / nRB;
+                            int rb = rest % nRB;
+                            if (!hasU) rb += BW;
+                            if (!hasC && rb >= BW) rb += BW;
+                            cb = rb;  // U blocks 0..BW-1, V blocks BW..2BW-1, b block 2BW
+                        }
+                        const int r0 = 6 * bi + 3 * h;
+                        double a[3][6], w[6][6];
 #pragma unroll
-                    for (int e = 0; e < 36; ++e) at[e] = -at[e];
+                        for (int rr = 0; rr < 3; ++rr) {
+                            const double2 *src = reinterpret_cast<const double2 *>(Dm + (r0 + rr) * S + 6 * k);
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) {
+                                const double2 v2 = src[c];
+                                a[rr][2 * c] = v2.x;
+                                a[rr][2 * c + 1] = v2.y;
+                            }
+                        }
+                        const int wc = isD ? 6 * cb : S + 6 * cb;
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) {
+                            const double2 *src = reinterpret_cast<const double2 *>(Wk + q * WS + wc);
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) {
+                                const double2 v2 = src[c];
+                                w[q][2 * c] = v2.x;
+                                w[q][2 * c + 1] = v2.y;
+                            }
+                        }
+                        double *dst = isD ? Dm + r0 * S + 6 * cb : Rm + r0 * RS + 6 * cb;
+                        const int ld = isD ? S : RS;
+#pragma unroll
+                        for (int rr = 0; rr < 3; ++rr) {
+                            double2 *o2 = reinterpret_cast<double2 *>(dst + rr * ld);
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) {
+                                double2 v2 = o2[c];
+                                double s0 = v2.x, s1 = v2.y;
+#pragma unroll
+                                for (int q = 0; q < 6; ++q) {
+                                    s0 = fma(-a[rr][q], w[q][2 * c], s0);
+                                    s1 = fma(-a[rr][q], w[q][2 * c + 1], s1);
+                                }
+                                o2[c] = make_double2(s0, s1);
+                            }
+                        }
+                    }
                 }
-                const int wc = role == 1 ? 6 * tj : S + 6 * tj;
-                lds_tile(Wm + (6 * k) * WS + wc, WS, bt);
-#pragma unroll
-                for (int ea = 0; ea < 6; ++ea)
-#pragma unroll
-                    for (int q = 0; q < 6; ++q)
-#pragma unroll
-                        for (int eb = 0; eb < 6; ++eb) acc[ea * 6 + eb] = fma(at[ea * 6 + q], bt[q * 6 + eb], acc[ea * 6 + eb]);
-                if (role == 1 && tj == k + 1) {
-                    lds_tile_store(Dm + (6 * ti) * S + 6 * tj, S, acc);
-                    if (ti == k + 1) factor_pivot(acc, pv + 48 * ((k + 1) & 1));  // next pivot block
-                }
-                if (role == 2 && ti == k + 1) lds_tile_store(Rm + (6 * ti) * RS + 6 * tj, RS, acc);
             }
             __syncthreads();
             BCR_STAMP(20 + k);
@@ -445,16 +518,31 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
         const uint32_t epoch = s_epoch;
         __syncthreads();
         const double fail_fwd = fail_in + (s_fail ? 1.0 : 0.0);  // meaningful on tid 0
-        // ---- publish the Gram tiles (element-major, coalesced write-through) + failure word
+        // ---- Gram G = R'ᵀ W_R (RS x RS) on v_mfma_f64_16x16x4f64: 16x16 tiles (I, J) with
+        //      J <= I + 1 (every 6x6 block (u, v) with u >= v lies in one), K = S in steps of 4.
+        //      Published write-through as 16x16 tiles, each row-major — the MFMA accumulator's own
+        //      lane order, so every store instruction is one contiguous 512-B run.
         if (!root) {
             double *pub = d.bcr_pub + (size_t)m * PUB;
-            if (role == 3) {
-                const int gt = tid - TRI - NRT;
-                const double sg = (ti >= BW && ti < 2 * BW && tj < BW) ? -1.0 : 1.0;  // F = -G_VU
+            const int wave = tid >> 6, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+            constexpr int NGT = bcr_gram_tiles(BW);
+            for (int gtl = wave; gtl < NGT; gtl += NT / 64) {
+                int I = 0, J = 0;
+                bcr_gram_tile(BW, gtl, I, J);
+                dbl4 acc4 = dbl4{0.0, 0.0, 0.0, 0.0};
+                const int p = 16 * I + lr, q = 16 * J + lr;
 #pragma unroll
-                for (int e = 0; e < 36; ++e) st_sc1(pub + (size_t)e * NG + gt, sg * acc[e]);
+                for (int ks = 0; ks < (S + 3) / 4; ++ks) {
+                    const int r = 4 * ks + lk;
+                    const double av = (r < S && p < RS) ? Rm[r * RS + p] : 0.0;       // A[p][r] = R'(r, p)
+                    const double bv = (r < S && q < RS) ? Wm[r * WS + S + q] : 0.0;   // B[r][q] = W(r, S + q)
+                    acc4 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc4, 0, 0, 0);
+                }
+                double *tp = pub + ((size_t)I * BCR_T16(BW) + J) * 256;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) st_sc1(tp + (lk + 4 * i) * 16 + lr, acc4[i]);
             }
-            if (tid == 0) st_sc1(pub + (size_t)36 * NG, fail_fwd);
+            if (tid == 0) st_sc1(pub + (size_t)BCR_T16(BW) * BCR_T16(BW) * 256, fail_fwd);
             bcr_publish(&d.bcr_flag[2 * m], epoch);
         }
         BCR_STAMP(13);

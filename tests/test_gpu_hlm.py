@@ -117,7 +117,8 @@ def test_hlm_rerun_is_bitwise_deterministic(solver):
         assert np.array_equal(a[k], b[k]), k
 
 
-GBA_CASES = [("C1L", {}), ("C2", {}), ("C2", {"lambda0": 1e-7, "err_per_obs": 1}), ("C3", {"max_iters": 6})]
+GBA_CASES = [("C1L", {}), ("C2", {}), ("C2", {"lambda0": 1e-7, "err_per_obs": 1}), ("C3", {"max_iters": 6}),
+             ("C3", {}), ("C4", {}), ("C4", {"lambda0": 1e-7, "err_per_obs": 1, "max_iters": 8})]
 
 
 @pytest.mark.parametrize("cfg,params", GBA_CASES, ids=[f"{c}-{'-'.join(f'{k}={v}' for k, v in p.items()) or 'ref'}"
