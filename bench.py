@@ -9,15 +9,20 @@ wall time. Workload (N=1): config C3 = 100 KF / 20k points / 4k lines (BASELINE.
 configs[2], the window north_star quotes its ≥50x target on).
 
 Multi-GPU (`--gpus N`, launched by torch.distributed.run), two modes:
-  --mode shard (default for N > 1)  ONE window split over the ranks by landmark:
+  --mode replicas (default)  every rank solves its own independent C3 window (different seed):
+                             a C3 window fits one GPU, and north_star shards a window only "when
+                             the window exceeds one GPU", so more GPUs = more windows, with no
+                             data-path collective (weak scaling; the same workload and unit as the
+                             N = 1 line). For N > 1 rank 0 then runs the sharded C5 job below as a
+                             child process group (bounded by a timeout, killed by its process
+                             group id if it overruns) and embeds its line as "shard_run".
+  --mode shard               ONE window split over the ranks by landmark:
                              BASELINE.json configs[4] (C5, 1000 KF, "report 1/2/4/8 scaling")
                              for every N > 1 (`--config C4` gives configs[3]); partial reduced
                              camera systems summed with RCCL all-reduces inside the captured step
                              graph (strong scaling); rank 0 also times the same window unsharded on
                              its GPU ("scaling_reference", the curve's 1-GPU point);
                              `--transport host` rehearses it with gloo.
-  --mode replicas            every rank solves its own independent C3 window (different seed):
-                             independent LBA windows need no data-path collective (weak scaling).
 The barrier and max-over-ranks timing use torch.distributed in both.
 
 Extra JSON objects:
@@ -56,8 +61,10 @@ def parse():
     p.add_argument("--cpu-runs", type=int, default=5)
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK (multi-rank rehearsal on 1 GPU)")
     p.add_argument("--mode", choices=["replicas", "shard"], default=None,
-                   help="default: replicas at N=1 (one C3 window), shard (C5) for N>1")
+                   help="default: replicas (one C3 window per GPU); shard: one C5 window over all ranks")
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="--mode shard all-reduce transport")
+    p.add_argument("--no-shard-run", action="store_true", help="replicas, N > 1: skip the embedded sharded C5 run")
+    p.add_argument("--shard-timeout", type=float, default=180.0, help="seconds allowed to the embedded sharded run")
     return p.parse_args()
 
 
@@ -136,6 +143,45 @@ def relaunch_distributed(a) -> int:
     return subprocess.run(cmd).returncode
 
 
+def shard_child(a, world: int):
+    """Rank 0 of a replicas job with N > 1: the sharded C5 strong-scaling job on the same N GPUs,
+    as a child process group (its own torch.distributed.run), after the replicas measurement. A
+    run that overruns --shard-timeout is killed by its process group id and reported as such; the
+    replicas line is printed either way."""
+    import signal
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                        "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("TORCHELASTIC_")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--mode", "shard",
+           "--steps", str(max(1, min(a.steps, 10))), "--warmup", "1", "--no-cpu-baseline",
+           "--transport", a.transport] + (["--device", str(a.device)] if a.device is not None else [])
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=a.shard_timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return {"error": f"timeout after {a.shard_timeout:.0f} s (process group killed)"}
+    wall = time.perf_counter() - t0
+    for line in reversed(out.splitlines()):
+        if line.startswith("{"):
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            keep = ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "scaling_reference",
+                    "final_chi2_gpu")
+            d = {k: r[k] for k in keep if k in r}
+            d["workload"] = r.get("config", {}).get("workload")
+            d["end_to_end"] = r.get("config", {}).get("end_to_end")
+            d["child_wall_s"] = wall
+            return d
+    return {"error": f"exit {p.returncode}, no JSON line", "stderr_tail": err[-2000:]}
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -155,7 +201,7 @@ def main():
     from plba.lib import Solver
 
     if a.mode is None:
-        a.mode = "shard" if world > 1 else "replicas"
+        a.mode = "replicas"
     shard = a.mode == "shard"
     if shard and "--config" not in sys.argv:
         # BASELINE.json configs[4]: the 1000-KF window, "report 1/2/4/8 scaling" — every N > 1
@@ -266,6 +312,13 @@ def main():
                            "speedup_of_this_run": (tot_iters / dt) / (ri / rdt)}
         dist.barrier()
 
+    # replicas, N > 1: the sharded C5 window on the same GPUs (child job; the other ranks wait)
+    shard_run = None
+    if not shard and world > 1 and not a.no_shard_run:
+        if rank == 0:
+            shard_run = shard_child(a, world)
+        dist.barrier()
+
     if rank == 0:
         # dominant kernel by device time in the instrumented step
         name, (kms, nl) = max(((k, v) for k, v in ktimes.items() if v[1] > 0), key=lambda kv: kv[1][0])
@@ -351,6 +404,8 @@ def main():
         out["final_chi2_gpu"] = [float(r["chi2"][0]), float(r["chi2"][1])]
         if scaling_ref is not None:
             out["scaling_reference"] = scaling_ref
+        if shard_run is not None:
+            out["shard_run"] = shard_run
         if world == 1 and not a.no_cpu_baseline:
             try:
                 cb = cpu_baseline(a.config, a.cpu_runs if a.config in ("C1", "C1L", "C2", "C3") else 1)

@@ -88,6 +88,8 @@ struct plba_ctx {
     size_t arena_cap = 0, staging_cap = 0;
     Ctrl *h_ctrl = nullptr;  // pinned
     uint8_t *d_depth = nullptr;  // [Ep] isDepthPositive flags
+    double *d_outd = nullptr;    // download staging, caller order: pt_xyz | ln_orth | χ² (points, lines)
+    uint8_t *d_outb = nullptr;   // depth flags [Ep] | levels (points, lines)
     // host-side bookkeeping
     int32_t n_kf = 0, n_pt = 0, n_ln = 0, Ep = 0, El = 0;
     std::vector<int32_t> e_orig;        // CSR edge -> original index within its type
@@ -1076,10 +1078,15 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ALLOC(d.red_rcs_loc, (size_t)nblk * 36 + (size_t)nf * 6);
         ALLOC(d.red_dec_loc, 3);  // + the hand-off error agreement slot (agree_dev_error)
     }
-    if (sharded) {  // final gather of the full window: X | χ² | depth | level
-        UPLOAD(d.lm_gpos, lm_gpos);
-        UPLOAD_D(d.e_gpos, e_gpos, wb.e_gpos, E);
+    // output maps (local landmark / edge -> whole-window position): the download scatter
+    // (k_out_scatter) or, sharded, the final gather of the full window X | χ² | depth | level
+    UPLOAD_D(d.lm_gpos, lm_gpos, wb.lm_gpos, n_lm);
+    UPLOAD_D(d.e_gpos, e_gpos, wb.e_gpos, E);
+    if (sharded) {
         ALLOC(d.gat, (size_t)(n_pt_g + n_ln_g) * 4 + 3 * (size_t)(Ep_g + El_g));
+    } else {
+        ALLOC(ctx->d_outd, (size_t)n_pt * 3 + (size_t)n_ln * 4 + E);
+        ALLOC(ctx->d_outb, (size_t)Ep + E);
     }
 #ifdef PLBA_STAMPS
     ZALLOC(d.stamps, 17 * 8);
@@ -1275,6 +1282,14 @@ int capture_steps(plba_ctx *ctx, int nsteps, hipGraph_t &graph, hipGraphExec_t &
 // Which kernels (template instances) a step launches, in which order: an executable graph is
 // updated in place only for a window with the same signature (hipGraphExecUpdate changes kernel
 // arguments and grids, never the kernel a node runs).
+// multi-step graphs captured: 2, 4, .. 2^L steps (PLBA_GRAPH_LEVELS overrides, for measurements)
+int graph_levels() {
+    static const int L = [] {
+        const char *e = getenv("PLBA_GRAPH_LEVELS");
+        return e ? std::max(0, std::min(atoi(e), (int)plba_ctx::kMultiLevels)) : (int)plba_ctx::kMultiLevels;
+    }();
+    return L;
+}
 std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
     const Dev &d = ctx->d;
     return {d.E > 0, d.nf > 0, d.n_lm > 0, d.n > 0, d.nch > 0, d.band_mode, d.dense_mfma, d.dense_mfma ? d.ntiles : 0,
@@ -1289,7 +1304,7 @@ int capture_step(plba_ctx *ctx) {
     ctx->graph_sig = sig;
     const auto t0 = std::chrono::steady_clock::now();
     int rc = capture_steps(ctx, 1, ctx->step_graph, ctx->step_exec);
-    for (int i = 0; i < plba_ctx::kMultiLevels && !rc; ++i)
+    for (int i = 0; i < graph_levels() && !rc; ++i)
         rc = capture_steps(ctx, 2 << i, ctx->multi_graph[i], ctx->multi_exec[i]);
     if (env_flag("PLBA_TIMING"))
         fprintf(stderr, "[plba upload] %-24s %8.3f ms\n", "graph capture",
@@ -1298,7 +1313,11 @@ int capture_step(plba_ctx *ctx) {
 }
 // launch n replays of the step as the binary decomposition of n over the captured graphs
 int launch_steps_graph(plba_ctx *ctx, int n) {
-    constexpr int L = plba_ctx::kMultiLevels;
+    const int L = graph_levels();
+    if (L == 0) {
+        for (int i = 0; i < n; ++i) PLBA_CHECK(hipGraphLaunch(ctx->step_exec, ctx->stream));
+        return PLBA_OK;
+    }
     while (n >= (2 << (L - 1))) {
         PLBA_CHECK(hipGraphLaunch(ctx->multi_exec[L - 1], ctx->stream));
         n -= 2 << (L - 1);
@@ -1506,6 +1525,37 @@ int gather_outputs(plba_ctx *ctx, std::vector<double> &out) {
     return PLBA_OK;
 }
 
+// Unsharded windows: every requested output in the caller's order, scattered on the device
+// (k_out_scatter) and copied straight into the caller's arrays, one synchronisation.
+int download_outputs(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth, double *ept_chi2,
+                     uint8_t *ept_depth_ok, double *eln_chi2, uint8_t *ept_level, uint8_t *eln_level) {
+    Dev &d = ctx->d;
+    hipStream_t s = ctx->stream;
+    const size_t np = (size_t)d.n_pt, nl = (size_t)d.n_ln, Ep = (size_t)d.Ep, El = (size_t)d.El;
+    const int m = std::max(d.n_lm, d.E);
+    const bool lm = pt_xyz || ln_orth, ed = ept_chi2 || ept_depth_ok || eln_chi2 || ept_level || eln_level;
+    if (m && (lm || ed)) {
+        hipLaunchKernelGGL(k_out_scatter, dim3(blocks_for(m)), dim3(kBlock), 0, s, d, ctx->d_outd, ctx->d_outb,
+                           ept_depth_ok ? 1 : 0);
+        PLBA_CHECK(hipGetLastError());
+    }
+    auto get = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+        return dst && bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s) : hipSuccess;
+    };
+    const double *od = ctx->d_outd;
+    const uint8_t *ob = ctx->d_outb;
+    PLBA_CHECK(get(kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12));
+    PLBA_CHECK(get(pt_xyz, od, sizeof(double) * np * 3));
+    PLBA_CHECK(get(ln_orth, od + np * 3, sizeof(double) * nl * 4));
+    PLBA_CHECK(get(ept_chi2, od + np * 3 + nl * 4, sizeof(double) * Ep));
+    PLBA_CHECK(get(eln_chi2, od + np * 3 + nl * 4 + Ep, sizeof(double) * El));
+    PLBA_CHECK(get(ept_depth_ok, ob, Ep));
+    PLBA_CHECK(get(ept_level, ob + Ep, Ep));
+    PLBA_CHECK(get(eln_level, ob + 2 * Ep, El));
+    PLBA_CHECK(hipStreamSynchronize(s));
+    return PLBA_OK;
+}
+
 }  // namespace
 
 // ==================================================================================== C ABI
@@ -1658,25 +1708,7 @@ int plba_get_edge_chi2(plba_ctx *ctx, double *ept_chi2, uint8_t *ept_depth_ok, d
         for (int e = 0; e < ctx->El && eln_chi2; ++e) eln_chi2[e] = o[ctx->Ep + e];
         return PLBA_OK;
     }
-    std::vector<double> chi(d.E);
-    std::vector<uint8_t> dep(d.Ep);
-    if (ept_depth_ok && d.Ep) {
-        hipLaunchKernelGGL(k_depth, dim3(blocks_for(d.Ep)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth);
-        PLBA_CHECK(hipGetLastError());
-        PLBA_CHECK(hipMemcpyAsync(dep.data(), ctx->d_depth, d.Ep, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    if (d.E) PLBA_CHECK(hipMemcpyAsync(chi.data(), d.chi2_last, sizeof(double) * d.E, hipMemcpyDeviceToHost, ctx->stream));
-    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
-    for (int e = 0; e < d.E; ++e) {
-        int o = ctx->e_orig[e];
-        if (e < d.Ep) {
-            if (ept_chi2) ept_chi2[o] = chi[e];
-            if (ept_depth_ok) ept_depth_ok[o] = dep[e];
-        } else if (eln_chi2) {
-            eln_chi2[o] = chi[e];
-        }
-    }
-    return PLBA_OK;
+    return download_outputs(ctx, nullptr, nullptr, nullptr, ept_chi2, ept_depth_ok, eln_chi2, nullptr, nullptr);
 }
 
 int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth) {
@@ -1695,21 +1727,7 @@ int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth
             for (int k = 0; k < 4; ++k) ln_orth[4 * l + k] = gv[(size_t)(ctx->n_pt + l) * 4 + k];
         return PLBA_OK;
     }
-    std::vector<double> X((size_t)d.n_lm * 4);
-    if (kf_Tcw && d.n_kf)
-        PLBA_CHECK(hipMemcpyAsync(kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost, ctx->stream));
-    if (d.n_lm) PLBA_CHECK(hipMemcpyAsync(X.data(), d.Xb[ctx->cur], sizeof(double) * X.size(), hipMemcpyDeviceToHost, ctx->stream));
-    PLBA_CHECK(hipStreamSynchronize(ctx->stream));
-    for (int i = 0; i < d.n_lm; ++i) {
-        const int gp = ctx->lm_gpos[i];
-        if (gp < ctx->n_pt) {
-            if (pt_xyz)
-                for (int k = 0; k < 3; ++k) pt_xyz[3 * (size_t)gp + k] = X[(size_t)i * 4 + k];
-        } else if (ln_orth) {
-            for (int k = 0; k < 4; ++k) ln_orth[4 * (size_t)(gp - ctx->n_pt) + k] = X[(size_t)i * 4 + k];
-        }
-    }
-    return PLBA_OK;
+    return download_outputs(ctx, kf_Tcw, pt_xyz, ln_orth, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 // The whole schedule of src/mapHandler.cpp:6119-6160 (stage 1, classification, stage 2,
@@ -1769,18 +1787,9 @@ int plba_lba_plucker(plba_ctx *ctx, plba_result *res) {
             }
             return PLBA_OK;
         }
-        if ((rc = plba_download(ctx, res->kf_Tcw, res->pt_xyz, res->ln_orth))) return rc;
-        if (res->ept_chi2 || res->ept_depth_ok || res->eln_chi2)
-            if ((rc = plba_get_edge_chi2(ctx, res->ept_chi2, res->ept_depth_ok, res->eln_chi2))) return rc;
-        if (res->ept_level || res->eln_level) {
-            std::vector<uint8_t> lv(d.E);
-            if (d.E) PLBA_CHECK(hipMemcpy(lv.data(), d.e_level, d.E, hipMemcpyDeviceToHost));
-            for (int e = 0; e < d.E; ++e) {
-                int o = ctx->e_orig[e];
-                if (e < d.Ep) { if (res->ept_level) res->ept_level[o] = lv[e]; }
-                else if (res->eln_level) res->eln_level[o] = lv[e];
-            }
-        }
+        if ((rc = download_outputs(ctx, res->kf_Tcw, res->pt_xyz, res->ln_orth, res->ept_chi2, res->ept_depth_ok,
+                                   res->eln_chi2, res->ept_level, res->eln_level)))
+            return rc;
     }
     return PLBA_OK;
 }

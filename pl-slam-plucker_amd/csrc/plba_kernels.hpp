@@ -2612,6 +2612,34 @@ __global__ void k_depth(Dev d, uint8_t *out) {
     out[e] = Pc[2] > 0.0 ? 1 : 0;
 }
 
+// unsharded download: landmark states and per-edge outputs in the caller's order (pt_xyz |
+// ln_orth | χ² by e_gpos, points then lines; bytes: isDepthPositive [Ep] | levels by e_gpos)
+__global__ void k_out_scatter(Dev d, double *od, uint8_t *ob, int want_depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d.n_lm) {
+        const int gp = d.lm_gpos[i];
+        const double *x = Xcur(d) + (size_t)i * 4;
+        if (gp < d.n_pt) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) od[(size_t)gp * 3 + k] = x[k];
+        } else {
+            double *o = od + (size_t)d.n_pt * 3 + (size_t)(gp - d.n_pt) * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] = x[k];
+        }
+    }
+    if (i < d.E) {
+        const int g = d.e_gpos[i];
+        od[(size_t)d.n_pt * 3 + (size_t)d.n_ln * 4 + g] = d.chi2_last[i];
+        ob[(size_t)d.Ep + g] = d.e_level[i];
+        if (want_depth && i < d.Ep) {
+            double Pc[3];
+            point_pc(Tcur(d) + (size_t)d.e_kf[i] * 12, Xcur(d) + (size_t)d.e_lm[i] * 4, Pc);
+            ob[g] = Pc[2] > 0.0 ? 1 : 0;
+        }
+    }
+}
+
 // sharded: scatter this rank's landmark states and per-edge outputs to their whole-window
 // positions (the buffer is zeroed first and summed over ranks afterwards)
 __global__ void k_gather(Dev d, const uint8_t *depth) {
