@@ -93,6 +93,7 @@ struct plba_ctx {
     // host-side bookkeeping
     int32_t n_kf = 0, n_pt = 0, n_ln = 0, Ep = 0, El = 0;
     std::vector<int32_t> e_orig;        // CSR edge -> original index within its type
+    std::vector<int32_t> h_tile_last;   // dense path: last row tile of each column tile's envelope
     std::vector<int32_t> lm_gpos;       // local landmark -> whole-window landmark (points, then lines)
     std::vector<uint8_t> h_level;       // [E] CSR order
     std::vector<plba_iter_trace> trace;
@@ -460,6 +461,7 @@ int collect_timing(plba_ctx *ctx) {
 // Reverse Cuthill–McKee order of the free poses (hidx 0..nf-1) on the graph "two free poses
 // observe a common landmark": BFS from a pseudo-peripheral vertex of each component, neighbours
 // by increasing degree, then reversed. Returns rcm[i] = the hidx placed at position i.
+std::vector<int32_t> rcm_from_adj(std::vector<std::vector<int32_t>> &adj);
 std::vector<int32_t> rcm_order(const plba_graph *g, const std::vector<int32_t> &kf_hidx, int nf) {
     const int nl = g->n_pt + g->n_ln;
     std::vector<std::vector<int32_t>> lm_poses(nl);
@@ -481,6 +483,11 @@ std::vector<int32_t> rcm_order(const plba_graph *g, const std::vector<int32_t> &
                 adj[v[j]].push_back(v[i]);
             }
     }
+    return rcm_from_adj(adj);
+}
+// RCM of an undirected graph given as adjacency lists (duplicates allowed; sorted in place)
+std::vector<int32_t> rcm_from_adj(std::vector<std::vector<int32_t>> &adj) {
+    const int nf = (int)adj.size();
     std::vector<int32_t> deg(nf);
     for (int h = 0; h < nf; ++h) {
         auto &a = adj[h];
@@ -886,6 +893,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             if (tile_first[I] <= K) last = I;
         tile_last[K] = last;
     }
+    ctx->h_tile_last = tile_last;
 
     mark("chunks + envelope");
     // ---- device allocation
@@ -1207,9 +1215,9 @@ int launch_step(plba_ctx *ctx) {
         if (d.band_mode) {
             LAUNCH(K_FACTOR, launch_band(d, s));
         } else if (d.dense_mfma) {  // blocked LDLᵀ, MFMA trailing updates (plba_dense.hpp)
-            for (int K = 0; K < d.ntiles; ++K) {
-                LAUNCH(K_DENSE_PANEL, hipLaunchKernelGGL(k_dense_panel, dim3((d.ntiles - K + 1) / 2), dim3(kDensePanelNT), 0, s, d, K));
-                const int m = d.ntiles - K - 1;
+            for (int K = 0; K < d.ntiles; ++K) {  // the envelope's row tiles K..tile_last[K] only
+                const int m = ctx->h_tile_last[K] - K;
+                LAUNCH(K_DENSE_PANEL, hipLaunchKernelGGL(k_dense_panel, dim3((m + 2) / 2), dim3(kDensePanelNT), 0, s, d, K));
                 if (m > 0)
                     LAUNCH(K_DENSE_UPDATE, hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, d, K));
             }
@@ -2180,6 +2188,42 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
             }
         }
     }
+    // ---- Hessian order: Cholmod orders H by AMD before its supernodal factorisation; here the
+    //      free vertices are reordered by reverse Cuthill–McKee when that narrows the band (loop
+    //      edges couple vertices far apart in id order), and the dense factorisation runs over the
+    //      envelope only (tile_first / tile_last). Any symmetric order gives the same exact solve.
+    std::vector<int32_t> first_h(nfree);
+    auto envelope_of = [&](const std::vector<int32_t> &hx, std::vector<int32_t> &fh) {
+        for (int h = 0; h < nfree; ++h) fh[h] = h;
+        for (int e : act) {
+            const int a = hx[g->e_v[2 * e]], b = hx[g->e_v[2 * e + 1]];
+            if (a < 0 || b < 0) continue;
+            fh[std::max(a, b)] = std::min(fh[std::max(a, b)], std::min(a, b));
+        }
+        int w = 0;
+        for (int h = 0; h < nfree; ++h) w = std::max(w, h - fh[h]);
+        return w;
+    };
+    {
+        int bwp = envelope_of(hidx, first_h);
+        if (bwp > 1 && nfree > 2 && !env_flag("PLBA_NO_RCM")) {
+            std::vector<std::vector<int32_t>> adj(nfree);
+            for (int e : act) {
+                const int a = hidx[g->e_v[2 * e]], b = hidx[g->e_v[2 * e + 1]];
+                if (a < 0 || b < 0 || a == b) continue;
+                adj[a].push_back(b);
+                adj[b].push_back(a);
+            }
+            const std::vector<int32_t> rcm = rcm_from_adj(adj);
+            std::vector<int32_t> pos(nfree), h2(nv, -1), fh2(nfree);
+            for (int i = 0; i < nfree; ++i) pos[rcm[i]] = i;
+            for (int v = 0; v < nv; ++v) h2[v] = hidx[v] >= 0 ? pos[hidx[v]] : -1;
+            if (envelope_of(h2, fh2) < bwp) {
+                hidx = h2;
+                first_h = fh2;
+            }
+        }
+    }
     // ---- blocks of H (lower triangle) and their contributions in edge order
     std::map<std::pair<int, int>, std::vector<int32_t>> blocks;  // (col, row) -> contributions
     for (int h = 0; h < nfree; ++h) blocks[{h, h}];
@@ -2254,7 +2298,18 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
         hiso_store(Zinv[e], &Zi[12 * (size_t)e]);
         for (int k = 0; k < 36; ++k) Om[36 * (size_t)e + k] = g->e_info ? g->e_info[36 * (size_t)e + k] : (k % 7 == 0 ? 1.0 : 0.0);
     }
-    std::vector<int32_t> tf(ntiles, 0), tl(ntiles, ntiles - 1);
+    std::vector<int32_t> tf(std::max(ntiles, 1), 0), tl(std::max(ntiles, 1), 0);
+    for (int I = 0; I < ntiles; ++I) {
+        int f = I;
+        for (int r = I * kTile; r < std::min(n, (I + 1) * kTile); ++r) f = std::min(f, (6 * first_h[r / 6]) / kTile);
+        tf[I] = f;
+    }
+    for (int K = 0; K < ntiles; ++K) {
+        int last = K;
+        for (int I = K; I < ntiles; ++I)
+            if (tf[I] <= K) last = I;
+        tl[K] = last;
+    }
     auto up = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
         return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
     };
@@ -2318,9 +2373,9 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
         do {
             // setLambda + solve (dense LDLᵀ, Cholmod's positive-definite test) + update
             hipLaunchKernelGGL(k_pgo_damp, dim3((unsigned)(((size_t)n * n + 255) / 256)), dim3(256), 0, s, P, Ad, lambda);
-            for (int K = 0; K < ntiles; ++K) {
-                hipLaunchKernelGGL(k_dense_panel, dim3((ntiles - K + 1) / 2), dim3(kDensePanelNT), 0, s, dd, K);
-                const int m = ntiles - K - 1;
+            for (int K = 0; K < ntiles; ++K) {  // the envelope's row tiles K..tl[K] only
+                const int m = tl[K] - K;
+                hipLaunchKernelGGL(k_dense_panel, dim3((m + 2) / 2), dim3(kDensePanelNT), 0, s, dd, K);
                 if (m > 0) hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, dd, K);
             }
             hipLaunchKernelGGL(k_pgo_check, dim3(1), dim3(256), 0, s, dd);

@@ -10,6 +10,9 @@
 //   k_dense_update<K>  one wave per trailing tile (I, J), K < J <= I: S_IJ -= W_IK·L_JKᵀ with
 //                      v_mfma_f64_16x16x4_f64 (2×2 blocks of 16×16, eight k-steps of 4), W and
 //                      L staged through LDS with coalesced loads.
+// Both launches cover only the envelope: row tiles up to tile_last[K], tiles whose row or column
+// envelope starts after K skipped (they are exact zeros — LDLᵀ makes no fill outside the
+// envelope), so an RCM-ordered matrix costs Σ_K (envelope height)² tiles, not (n/32)³/6.
 // The forward substitution L y = b rides along: panel K solves y_K = L_KK⁻¹ b_K on its diagonal
 // tile and the diagonal update tile (I, I) of step K subtracts L_IK·y_K from b_I (dense_yd).
 // Then k_dense_solve: D⁻¹ and the backward substitution through the factor (one workgroup,
@@ -85,7 +88,8 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
         }
         if (ok && lane < 32) {  // forward substitution of tile K: y_K = L_KK⁻¹ b_K
             double *yd = dense_yd(d);
-            double yi = (K == 0 ? d.bs : yd)[k0 + min(r, kb - 1)];
+            // (rows of tile K first touched here when its envelope starts at K)
+            double yi = (d.tile_first[K] == K ? d.bs : yd)[k0 + min(r, kb - 1)];
 #pragma unroll
             for (int j = 0; j < kDT; ++j) {
                 const double yj = readlane_f64(yi, j);
@@ -95,7 +99,8 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
         }
     }
     DENSE_STAMP(4);
-    if (!ok || I == K || I >= d.ntiles) return;
+    // row tiles outside the envelope of column tile K: S_IK = 0, so W_IK = L_IK = 0 (never read)
+    if (!ok || I == K || I > d.tile_last[K] || d.tile_first[I] > K) return;
     const bool live = i0 + r < n;
     double a[kDT];
     {
@@ -140,6 +145,8 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
     const int lane = threadIdx.x, n = d.n;
     int I, J;
     dense_tile_of(blockIdx.x, K, I, J);
+    // envelope: L_IK or L_JK is zero — nothing to subtract (the grid covers K < J <= I <= tile_last[K])
+    if (d.tile_first[I] > K || d.tile_first[J] > K) return;
     const int k0 = K * kDT, kb = min(kDT, n - k0);
     const int i0 = I * kDT, j0 = J * kDT;
     const double *Ad = d.Ad;
@@ -190,7 +197,7 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
 #pragma unroll
         for (int p = 0; p < kDT; ++p)
             if (p < kb) s += Ls[lane][p] * yk[p];
-        yd[i0 + lane] = (K == 0 ? d.bs : yd)[i0 + lane] - s;
+        yd[i0 + lane] = (K == d.tile_first[I] ? d.bs : yd)[i0 + lane] - s;  // first update of rows I
     }
     double *Aw = d.Ad;
     double cv[2][2][4];  // the 16 entries of C this lane updates: all loads, then all stores
