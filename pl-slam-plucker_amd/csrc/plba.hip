@@ -88,8 +88,10 @@ struct plba_ctx {
     size_t arena_cap = 0, staging_cap = 0;
     Ctrl *h_ctrl = nullptr;  // pinned
     uint8_t *d_depth = nullptr;  // [Ep] isDepthPositive flags
-    double *d_outd = nullptr;    // download staging, caller order: pt_xyz | ln_orth | χ² (points, lines)
-    uint8_t *d_outb = nullptr;   // depth flags [Ep] | levels (points, lines)
+    double *d_outd = nullptr;    // download staging, caller order: Tcw | pt_xyz | ln_orth | χ² (points,
+                                 // lines) | bytes: depth flags [Ep] | levels (points, lines)
+    char *h_out = nullptr;       // pinned host copy of it (grow-only)
+    size_t h_out_cap = 0;
     // host-side bookkeeping
     int32_t n_kf = 0, n_pt = 0, n_ln = 0, Ep = 0, El = 0;
     std::vector<int32_t> e_orig;        // CSR edge -> original index within its type
@@ -462,6 +464,8 @@ int collect_timing(plba_ctx *ctx) {
 // observe a common landmark": BFS from a pseudo-peripheral vertex of each component, neighbours
 // by increasing degree, then reversed. Returns rcm[i] = the hidx placed at position i.
 std::vector<int32_t> rcm_from_adj(std::vector<std::vector<int32_t>> &adj);
+// doubles of the download staging block before its byte outputs
+inline size_t out_doubles(size_t n_kf, size_t n_pt, size_t n_ln, size_t E) { return n_kf * 12 + n_pt * 3 + n_ln * 4 + E; }
 std::vector<int32_t> rcm_order(const plba_graph *g, const std::vector<int32_t> &kf_hidx, int nf) {
     const int nl = g->n_pt + g->n_ln;
     std::vector<std::vector<int32_t>> lm_poses(nl);
@@ -1093,8 +1097,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     if (sharded) {
         ALLOC(d.gat, (size_t)(n_pt_g + n_ln_g) * 4 + 3 * (size_t)(Ep_g + El_g));
     } else {
-        ALLOC(ctx->d_outd, (size_t)n_pt * 3 + (size_t)n_ln * 4 + E);
-        ALLOC(ctx->d_outb, (size_t)Ep + E);
+        // one staging block: Tcw | pt_xyz | ln_orth | χ² (doubles), then the byte outputs
+        ALLOC(ctx->d_outd, out_doubles(n_kf, n_pt, n_ln, E) + ((size_t)Ep + E + 7) / 8);
     }
 #ifdef PLBA_STAMPS
     ZALLOC(d.stamps, 17 * 8);
@@ -1396,7 +1400,11 @@ int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
     }
     // the host transport synchronises inside the step: no graph then
     bool use_graph = !ctx->timing && ctx->comm.kind != plba_ctx::Comm::HOST && !ctx->no_graph;
-    if (use_graph) {
+    // A new window's step graphs are captured (or updated) on the host while the device runs the
+    // first batch, launched directly: the capture leaves the end-to-end call's critical path.
+    bool capture_pending = use_graph && (!ctx->step_exec || ctx->graphs_stale);
+    auto capture_now = [&]() -> int {
+        capture_pending = false;
         int rc = capture_step(ctx);
         if (rc && ctx->comm.kind == plba_ctx::Comm::RCCL) {
             // collectives that refuse stream capture: fall back to direct launches for good
@@ -1405,15 +1413,17 @@ int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
             use_graph = false;
             if (ctx->opts.verbose) fprintf(stderr, "[plba] step capture with RCCL failed (%s); direct launches\n",
                                            ctx->err.c_str());
-        } else if (rc) {
-            return rc;
+            return PLBA_OK;
         }
-    }
+        return rc;
+    };
     int launched = 0;
     int batch = std::max(4, ctx->last_steps);
+    const bool tlog = env_flag("PLBA_TIMING");
+    auto tb0 = std::chrono::steady_clock::now();
     const int max_steps = init.n_stages * 10 * (init.max_iters[0] + init.max_iters[1] + 2) + 8;
     for (;;) {
-        if (use_graph) {
+        if (use_graph && !capture_pending) {
             int rc = launch_steps_graph(ctx, batch);
             if (rc) return rc;
         } else {
@@ -1421,10 +1431,18 @@ int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
                 int rc = launch_step(ctx);
                 if (rc) return rc;
             }
+            if (capture_pending)
+                if (int rc = capture_now()) return rc;
         }
         launched += batch;
         int rc = read_ctrl(ctx);
         if (rc) return rc;
+        if (tlog) {
+            const auto tb1 = std::chrono::steady_clock::now();
+            fprintf(stderr, "[plba schedule] batch of %3d steps (%3d so far, device step %3d) %8.3f ms\n", batch, launched,
+                    ctx->h_ctrl->steps, std::chrono::duration<double, std::milli>(tb1 - tb0).count());
+            tb0 = tb1;
+        }
         int any_error = ctx->h_ctrl->dev_error;
         if (d.sharded && d.bcr && (rc = agree_dev_error(ctx, any_error, &any_error))) return rc;
         if (any_error) {
@@ -1534,33 +1552,43 @@ int gather_outputs(plba_ctx *ctx, std::vector<double> &out) {
 }
 
 // Unsharded windows: every requested output in the caller's order, scattered on the device
-// (k_out_scatter) and copied straight into the caller's arrays, one synchronisation.
+// (k_out_scatter) into one staging block, one copy into pinned memory, one synchronisation, then
+// host copies into the caller's arrays.
 int download_outputs(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth, double *ept_chi2,
                      uint8_t *ept_depth_ok, double *eln_chi2, uint8_t *ept_level, uint8_t *eln_level) {
     Dev &d = ctx->d;
     hipStream_t s = ctx->stream;
-    const size_t np = (size_t)d.n_pt, nl = (size_t)d.n_ln, Ep = (size_t)d.Ep, El = (size_t)d.El;
-    const int m = std::max(d.n_lm, d.E);
-    const bool lm = pt_xyz || ln_orth, ed = ept_chi2 || ept_depth_ok || eln_chi2 || ept_level || eln_level;
-    if (m && (lm || ed)) {
-        hipLaunchKernelGGL(k_out_scatter, dim3(blocks_for(m)), dim3(kBlock), 0, s, d, ctx->d_outd, ctx->d_outb,
-                           ept_depth_ok ? 1 : 0);
-        PLBA_CHECK(hipGetLastError());
+    const size_t nk = (size_t)d.n_kf, np = (size_t)d.n_pt, nl = (size_t)d.n_ln, Ep = (size_t)d.Ep, El = (size_t)d.El;
+    const size_t nd = out_doubles(nk, np, nl, Ep + El), bytes = nd * sizeof(double) + Ep + (Ep + El);
+    const int m = std::max({d.n_lm, d.E, d.n_kf});
+    const bool any = kf_Tcw || pt_xyz || ln_orth || ept_chi2 || ept_depth_ok || eln_chi2 || ept_level || eln_level;
+    if (!m || !any) return PLBA_OK;
+    if (bytes > ctx->h_out_cap) {  // grow-only, with slack: the next windows of a session are similar
+        if (ctx->h_out) (void)hipHostFree(ctx->h_out);
+        ctx->h_out = nullptr;
+        ctx->h_out_cap = 0;
+        const size_t cap = bytes + bytes / 2;
+        PLBA_CHECK(hipHostMalloc((void **)&ctx->h_out, cap));
+        ctx->h_out_cap = cap;
     }
-    auto get = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
-        return dst && bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s) : hipSuccess;
-    };
-    const double *od = ctx->d_outd;
-    const uint8_t *ob = ctx->d_outb;
-    PLBA_CHECK(get(kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12));
-    PLBA_CHECK(get(pt_xyz, od, sizeof(double) * np * 3));
-    PLBA_CHECK(get(ln_orth, od + np * 3, sizeof(double) * nl * 4));
-    PLBA_CHECK(get(ept_chi2, od + np * 3 + nl * 4, sizeof(double) * Ep));
-    PLBA_CHECK(get(eln_chi2, od + np * 3 + nl * 4 + Ep, sizeof(double) * El));
-    PLBA_CHECK(get(ept_depth_ok, ob, Ep));
-    PLBA_CHECK(get(ept_level, ob + Ep, Ep));
-    PLBA_CHECK(get(eln_level, ob + 2 * Ep, El));
+    hipLaunchKernelGGL(k_out_scatter, dim3(blocks_for(m)), dim3(kBlock), 0, s, d, ctx->d_outd, ept_depth_ok ? 1 : 0,
+                       ctx->cur);
+    PLBA_CHECK(hipGetLastError());
+    PLBA_CHECK(hipMemcpyAsync(ctx->h_out, ctx->d_outd, bytes, hipMemcpyDeviceToHost, s));
     PLBA_CHECK(hipStreamSynchronize(s));
+    const double *od = reinterpret_cast<const double *>(ctx->h_out);
+    const uint8_t *ob = reinterpret_cast<const uint8_t *>(od + nd);
+    auto put = [](void *dst, const void *src, size_t b) {
+        if (dst && b) std::memcpy(dst, src, b);
+    };
+    put(kf_Tcw, od, sizeof(double) * nk * 12);
+    put(pt_xyz, od + nk * 12, sizeof(double) * np * 3);
+    put(ln_orth, od + nk * 12 + np * 3, sizeof(double) * nl * 4);
+    put(ept_chi2, od + nk * 12 + np * 3 + nl * 4, sizeof(double) * Ep);
+    put(eln_chi2, od + nk * 12 + np * 3 + nl * 4 + Ep, sizeof(double) * El);
+    put(ept_depth_ok, ob, Ep);
+    put(ept_level, ob + Ep, Ep);
+    put(eln_level, ob + 2 * Ep, El);
     return PLBA_OK;
 }
 
@@ -1616,6 +1644,7 @@ int plba_destroy(plba_ctx *ctx) {
     ctx->bmemA.release();
     ctx->bmemB.release();
     if (ctx->pgo_hout) (void)hipHostFree(ctx->pgo_hout);
+    if (ctx->h_out) (void)hipHostFree(ctx->h_out);
     if (ctx->comm.hbuf) (void)hipHostFree(ctx->comm.hbuf);
     if (ctx->comm.nccl) (void)ncclCommDestroy(ctx->comm.nccl);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -2612,29 +2612,37 @@ __global__ void k_depth(Dev d, uint8_t *out) {
     out[e] = Pc[2] > 0.0 ? 1 : 0;
 }
 
-// unsharded download: landmark states and per-edge outputs in the caller's order (pt_xyz |
-// ln_orth | χ² by e_gpos, points then lines; bytes: isDepthPositive [Ep] | levels by e_gpos)
-__global__ void k_out_scatter(Dev d, double *od, uint8_t *ob, int want_depth) {
+// unsharded download: poses, landmark states and per-edge outputs in the caller's order, one
+// staging block (Tcw | pt_xyz | ln_orth | χ² by e_gpos, points then lines | bytes:
+// isDepthPositive [Ep] | levels by e_gpos)
+__global__ void k_out_scatter(Dev d, double *od, int want_depth, int cur) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const double *T = d.Tb[cur], *X = d.Xb[cur];  // the host's current state index
+    const size_t nk = d.n_kf, np = d.n_pt, nl = d.n_ln, E = d.E;
+    if (i < d.n_kf)
+#pragma unroll
+        for (int k = 0; k < 12; ++k) od[(size_t)i * 12 + k] = T[(size_t)i * 12 + k];
+    double *opt = od + nk * 12;
     if (i < d.n_lm) {
         const int gp = d.lm_gpos[i];
-        const double *x = Xcur(d) + (size_t)i * 4;
+        const double *x = X + (size_t)i * 4;
         if (gp < d.n_pt) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) od[(size_t)gp * 3 + k] = x[k];
+            for (int k = 0; k < 3; ++k) opt[(size_t)gp * 3 + k] = x[k];
         } else {
-            double *o = od + (size_t)d.n_pt * 3 + (size_t)(gp - d.n_pt) * 4;
+            double *o = opt + np * 3 + (size_t)(gp - d.n_pt) * 4;
 #pragma unroll
             for (int k = 0; k < 4; ++k) o[k] = x[k];
         }
     }
     if (i < d.E) {
         const int g = d.e_gpos[i];
-        od[(size_t)d.n_pt * 3 + (size_t)d.n_ln * 4 + g] = d.chi2_last[i];
+        opt[np * 3 + nl * 4 + g] = d.chi2_last[i];
+        uint8_t *ob = reinterpret_cast<uint8_t *>(opt + np * 3 + nl * 4 + E);
         ob[(size_t)d.Ep + g] = d.e_level[i];
         if (want_depth && i < d.Ep) {
             double Pc[3];
-            point_pc(Tcur(d) + (size_t)d.e_kf[i] * 12, Xcur(d) + (size_t)d.e_lm[i] * 4, Pc);
+            point_pc(T + (size_t)d.e_kf[i] * 12, X + (size_t)d.e_lm[i] * 4, Pc);
             ob[g] = Pc[2] > 0.0 ? 1 : 0;
         }
     }
