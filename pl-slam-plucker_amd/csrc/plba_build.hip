@@ -74,13 +74,45 @@ __global__ void k_b_edges(Raw r, int32_t *first_e, int32_t *cnt, int32_t *lmin, 
     if (h >= 0) atomicMin(&lmin[lm], h);
 }
 // envelope over the WHOLE window (every rank of a sharded window needs one layout)
-__global__ void k_b_first_blk(Raw r, const int32_t *lmin, int32_t *first_blk) {
-    const int e = blockIdx.x * kNT + threadIdx.x;
-    if (e >= r.Ep + r.El) return;
-    int lm, kf;
-    edge_of(r, e, lm, kf);
-    const int h = r.kf_hidx[kf];
-    if (h >= 0) atomicMin(&first_blk[h], lmin[lm]);
+// envelope: first_blk[h] = min over the edges at free pose h of lmin[landmark]. Thousands of edges
+// share a pose, so the minimum is taken in LDS first (one copy per workgroup, a grid-stride run of
+// edges each) and each workgroup folds its copy into the global one: a few global atomics per
+// pose instead of one per edge (min is order-independent: the result is the same).
+constexpr int kFirstBlkLds = 8192;
+__global__ void k_b_first_blk(Raw r, const int32_t *lmin, int32_t *first_blk, int nf) {
+    __shared__ int32_t sm[kFirstBlkLds];
+    const int E = r.Ep + r.El;
+    const bool lds = nf <= kFirstBlkLds;
+    if (lds) {
+        for (int h = threadIdx.x; h < nf; h += kNT) sm[h] = INT32_MAX;
+        __syncthreads();
+    }
+    for (int e = blockIdx.x * kNT + threadIdx.x; e < E; e += gridDim.x * kNT) {
+        int lm, kf;
+        edge_of(r, e, lm, kf);
+        const int h = r.kf_hidx[kf];
+        if (h < 0) continue;
+        if (lds) atomicMin(&sm[h], lmin[lm]);
+        else atomicMin(&first_blk[h], lmin[lm]);
+    }
+    if (lds) {
+        __syncthreads();
+        for (int h = threadIdx.x; h < nf; h += kNT)
+            if (sm[h] != INT32_MAX) atomicMin(&first_blk[h], sm[h]);
+    }
+}
+// off[b] = number of keys < b in a sorted key array (b = 0..nb): the exclusive scan of the
+// per-key counts, by binary search instead of one atomic per element
+__global__ void k_b_lbound(const uint32_t *key, int64_t n, int nb, int32_t *off) {
+    const int b = blockIdx.x * kNT + threadIdx.x;
+    if (b > nb) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (key[mid] < (uint32_t)b) lo = mid + 1;
+        else hi = mid;
+    }
+    off[b] = (int32_t)lo;
 }
 __global__ void k_b_iota(int32_t *a, int n) {
     const int i = blockIdx.x * kNT + threadIdx.x;
@@ -208,7 +240,7 @@ __global__ void k_b_pekey(const int32_t *e_hidx, const int32_t *lm_off, const in
     const int h = i < E ? e_hidx[i] : -1;
     key[i] = h >= 0 ? (uint32_t)h : (uint32_t)nf;
     val[i] = i;
-    if (h >= 0) atomicAdd(&pcnt[h], 1);
+    (void)pcnt;
 }
 __global__ void k_b_summary(const int32_t *info, const int32_t *lm_off, const int32_t *pe_off, int nf, int32_t *out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -252,10 +284,6 @@ __global__ void k_b_tfill(const int32_t *lm_off, const int32_t *e_hidx, const in
             ++t;
         }
     }
-}
-__global__ void k_b_hist(const uint32_t *key, int64_t n, int32_t *cnt) {
-    const int64_t t = (int64_t)blockIdx.x * kNT + threadIdx.x;
-    if (t < n) atomicAdd(&cnt[key[t]], 1);
 }
 
 #define BCHECK(expr)                                                                                 \
@@ -408,7 +436,9 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
         return PLBA_E_INVALID;
     }
     hipLaunchKernelGGL(k_b_iota, dim3(grid(nf)), dim3(kNT), 0, st, s.first_blk, nf);
-    if (E) hipLaunchKernelGGL(k_b_first_blk, dim3(grid(E)), dim3(kNT), 0, st, r, s.lmin, s.first_blk);
+    if (E && nf)
+        hipLaunchKernelGGL(k_b_first_blk, dim3((unsigned)std::min<int64_t>(grid(E), 64)), dim3(kNT), 0, st, r, s.lmin,
+                           s.first_blk, nf);
     BCHECK(hipGetLastError());
     size_t tb = s.temp_bytes;
     if (L > 0) {
@@ -451,8 +481,10 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
         BCHECK(rocprim::radix_sort_pairs(s.temp, tb, s.pkey, s.pkey2, s.pval, s.pval2, (size_t)E, 0, bits_for(nf), st));
     }
     if (L) hipLaunchKernelGGL(k_b_states, dim3(grid(L)), dim3(kNT), 0, st, r, s.lm_gpos, s.info, s.X);
-    tb = s.temp_bytes;
-    BCHECK(rocprim::exclusive_scan(s.temp, tb, s.pcnt, s.pe_off, 0, (size_t)nf + 1, rocprim::plus<int32_t>(), st));
+    // free-pose CSR offsets from the sorted pose keys (non-free edges carry key nf, sorted last)
+    if (E) hipLaunchKernelGGL(k_b_lbound, dim3(grid((int64_t)nf + 1)), dim3(kNT), 0, st, s.pkey2, (int64_t)E, nf, s.pe_off);
+    else BCHECK(hipMemsetAsync(s.pe_off, 0, sizeof(int32_t) * (nf + 1), st));
+    BCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_b_summary, dim3(1), dim3(64), 0, st, s.info, s.lm_off, s.pe_off, nf, s.summary);
     BCHECK(hipGetLastError());
     // ---- read back the counts, the first invalid edge and the envelope
@@ -522,18 +554,18 @@ int build_stage2(BuildMem &A, BuildMem &B, WindowBuild &wb, const std::vector<in
     }
     Carver c2{B.base};
     layout(c2, k1, k2, v1, v2, bc, bo, tp);
-    BCHECK(hipMemsetAsync(bc, 0, sizeof(int32_t) * ((size_t)nblk + 1), st));
     if (T > 0) {
         hipLaunchKernelGGL(k_b_tfill, dim3(grid(NL)), dim3(kNT), 0, st, s.lm_off, s.e_hidx, s.toff, s.blk_base,
                            s.first_blk, NL, k1, v1);
         BCHECK(hipGetLastError());
         tb = tmp;
         BCHECK(rocprim::radix_sort_pairs(tp, tb, k1, k2, v1, v2, (size_t)T, 0, bits_for(nblk), st));
-        hipLaunchKernelGGL(k_b_hist, dim3(grid(T)), dim3(kNT), 0, st, k2, T, bc);
-        BCHECK(hipGetLastError());
     }
-    tb = tmp;
-    BCHECK(rocprim::exclusive_scan(tp, tb, bc, bo, 0, (size_t)nblk + 1, rocprim::plus<int32_t>(), st));
+    // block offsets from the sorted block keys
+    if (T > 0) hipLaunchKernelGGL(k_b_lbound, dim3(grid((int64_t)nblk + 1)), dim3(kNT), 0, st, k2, T, nblk, bo);
+    else BCHECK(hipMemsetAsync(bo, 0, sizeof(int32_t) * ((size_t)nblk + 1), st));
+    BCHECK(hipGetLastError());
+    (void)bc;
     wb.h_blk_off.assign((size_t)nblk + 1, 0);
     BCHECK(hipMemcpyAsync(wb.h_blk_off.data(), bo, sizeof(int32_t) * ((size_t)nblk + 1), hipMemcpyDeviceToHost, st));
     BCHECK(hipStreamSynchronize(st));
