@@ -26,12 +26,13 @@ for cfg in sys.argv[1:] or ["C1", "C2", "C3", "C4", "C5"]:
     g = synth.generate(cfg)
     prev = os.sched_getaffinity(0)
     os.sched_setaffinity(0, {min(prev)})
-    nrun = 3 if cfg in ("C1", "C1L", "C2", "C3") else 1
+    nrun = 3  # median of 3 everywhere (single C5 runs differed by 31 %)
     oa.lba_plucker(g)
     cms = []
     for _ in range(nrun):
         ref = oa.lba_plucker(g)
         cms.append(ref["solve_ms"])
+        print(f"# {cfg} cpu run {len(cms)}: {ref['solve_ms']:.1f} ms", file=sys.stderr, flush=True)
     os.sched_setaffinity(0, prev)
     cit = int(ref["iters"][0] + ref["iters"][1])
     with Solver() as s:
@@ -49,7 +50,7 @@ for cfg in sys.argv[1:] or ["C1", "C2", "C3", "C4", "C5"]:
     c_ms_it = statistics.median(cms) / cit
     g_ms_it = statistics.median(gms) / git
     B = synth.algorithmic_bytes_per_iter(g)
-    rows.append(dict(cfg=cfg, cpu_ms_it=c_ms_it, gpu_ms_it=g_ms_it, speedup=c_ms_it / g_ms_it,
+    rows.append(dict(cfg=cfg, cpu_ms_it=c_ms_it, cpu_ms_runs=[round(x, 1) for x in cms], gpu_ms_it=g_ms_it, speedup=c_ms_it / g_ms_it,
                      chi2_cpu=float(ref["chi2"][1]), chi2_gpu=float(out["chi2"][1]),
                      max_rel=max(m["Tcw"], m["pt"], m["ln"]), hbm_frac=B / (g_ms_it * 1e-3) / 1e9 / HBM,
                      factor="bcr" if st["bcr_rows"] else ("column-lane" if st["column_lane"] else "band/dense"),
