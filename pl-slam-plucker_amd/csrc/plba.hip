@@ -1406,16 +1406,18 @@ int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
     auto capture_now = [&]() -> int {
         capture_pending = false;
         int rc = capture_step(ctx);
-        if (rc && ctx->comm.kind == plba_ctx::Comm::RCCL) {
-            // collectives that refuse stream capture: fall back to direct launches for good
+        if (rc) {
+            // a step that cannot be captured (collectives that refuse stream capture, graph
+            // instantiation failing for lack of memory): the first batch is already running as
+            // direct launches, so keep launching that way for the rest of this context's life
             (void)hipGetLastError();
+            destroy_graphs(ctx);
             ctx->no_graph = true;
             use_graph = false;
-            if (ctx->opts.verbose) fprintf(stderr, "[plba] step capture with RCCL failed (%s); direct launches\n",
-                                           ctx->err.c_str());
-            return PLBA_OK;
+            if (ctx->opts.verbose) fprintf(stderr, "[plba] step capture failed (%s); direct launches\n", ctx->err.c_str());
+            ctx->err.clear();
         }
-        return rc;
+        return PLBA_OK;
     };
     int launched = 0;
     int batch = std::max(4, ctx->last_steps);
