@@ -105,3 +105,13 @@ def test_pgo_solve_with_y_in_global_memory(solver, monkeypatch):
     out = solver.pgo_optimize(pg)
     np.testing.assert_array_equal(out["v_T"], lds["v_T"])
     _compare(out, oa.pgo_optimize(pg))
+
+
+def test_pgo_id_order_full_envelope_matches_oracle(solver, monkeypatch):
+    """PLBA_NO_RCM=1: the Hessian in g2o's id order with the loop edges' full envelope (the dense
+    factorisation over every tile), same oracle agreement as the RCM-ordered default."""
+    monkeypatch.setenv("PLBA_NO_RCM", "1")
+    pg = pgo.loop_graph(n_kf=150, seed=9, cov_window=4, extra_loops=6)
+    ref = oa.pgo_optimize(pg)
+    out = solver.pgo_optimize(pg)
+    _compare(out, ref)
