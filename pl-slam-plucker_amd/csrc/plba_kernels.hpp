@@ -879,13 +879,17 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
 #pragma unroll
     for (int k = 0; k < 42; ++k) acc[k] = 0.0;
     const int t0 = d.ch_off[ch], t1 = d.ch_off[ch + 1];
+    // the next batch's triple indices are loaded one batch ahead, so their latency hides behind
+    // this batch's row loads instead of preceding them (rows past the chunk re-read a valid triple)
+    int2 nx = make_int2(0, 0);
+    if (t0 < t1) nx = reinterpret_cast<const int2 *>(d.trip)[min(t0 + lane, t1 - 1)];
 #pragma unroll 1
     for (int q = 0; q < kChunk / 64; ++q) {
         const int tb = t0 + 64 * q;
         if (tb >= t1) break;  // wave-uniform
         const int t = tb + lane;
-        const int tt = t < t1 ? t : tb;  // rows past the chunk fetch a valid edge, add nothing
-        const int e1 = d.trip[2 * tt], e2 = d.trip[2 * tt + 1];
+        const int e1 = nx.x, e2 = nx.y;
+        if (tb + 64 < t1) nx = reinterpret_cast<const int2 *>(d.trip)[min(tb + 64 + lane, t1 - 1)];
         double z1[8], z2[8], a1[12], a2[12];
         if (STAGED) {
             dbl2 *sA1 = reinterpret_cast<dbl2 *>(smem), *sA2 = sA1 + 384;
