@@ -332,6 +332,11 @@ inline bool use_cl(int bw) {
     if (f && std::string(f) == "band") return false;
     return bw >= 1 && bw <= kClMaxBW && !env_flag("PLBA_NO_CL");
 }
+// Two-sided split: rows 0..m-1 top-down, nf-1..m+bw bottom-up. An odd remainder goes to the top
+// segment, so workgroup 0 usually arrives last and merges with the separator window already in
+// its LDS (workgroup 1 as the last arriver must first reload segment 0's window from global
+// memory): C3 hand-off + merge 10.9 k -> 8.1 k cycles, factorisation 74.8 -> 73.3 µs.
+inline int tw_split(int nf, int bw) { return (nf - bw + 1) / 2; }
 inline size_t cl_lds_bytes(int bw, int nf, bool twisted) {
     return sizeof(double) * (cl_lds_doubles(bw) + (twisted ? (size_t)nf * 6 : 0));
 }
@@ -931,10 +936,10 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     const bool fb_tw = bcr && use_cl(bw) && nf >= 2 * bw + 16 && cl_lds_bytes(bw, nf, true) <= 159 * 1024 &&
                        !(no_twist && no_twist[0] == '1');
     ctx->fb_twisted = fb_tw ? 1 : 0;
-    ctx->fb_tw_m = fb_tw ? (nf - bw) / 2 : 0;
+    ctx->fb_tw_m = fb_tw ? tw_split(nf, bw) : 0;
     d.cl = cl && cl_lds_bytes(bw, nf, twisted) <= 159 * 1024 ? 1 : 0;
     d.twisted = twisted ? 1 : 0;
-    d.tw_m = twisted ? (nf - bw) / 2 : 0;
+    d.tw_m = twisted ? tw_split(nf, bw) : 0;
     d.corrected = ctx->opts.corrected_line_jacobian;
     {  // timing experiments only (wrong results): PLBA_DIAG bit mask read by some kernels
         const char *dg = getenv("PLBA_DIAG");

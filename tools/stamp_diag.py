@@ -22,7 +22,7 @@ names = ["top(prefetch)", "phase1", "bar1", "ph2-end(refill|crit)", "bar2", "ph2
 ntr = int(sum(t["trials"] for t in out["trace"]))
 nf = int((g.kf_fixed == 0).sum())
 st = s.structure_stats()
-steps_per_trial = (nf - st["bw"]) // 2 if st["twisted"] else nf
+steps_per_trial = (nf - st["bw"] + 1) // 2 if st["twisted"] else nf
 print(cfg, "rc", rc, "trials", ntr, "forward steps per trial", steps_per_trial, "twisted", st["twisted"])
 if st.get("column_lane"):
     names = ["A:publish", "B:gauss-jordan", "C:publish-X", "barrier", "EF:next-column", "prefetch",

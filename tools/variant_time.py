@@ -22,7 +22,8 @@ def child(cfg: str, libname: str):
     ms = []
     for _ in range(6):
         s.reset()
-        ms.append(s.lba_plucker(want_outputs=False)["solve_ms"])
+        r = s.lba_plucker(want_outputs=False)
+        ms.append(r["solve_ms"])
     s.close()
     t = lib.Solver(kernel_timing=True)
     t.upload(g)
@@ -31,6 +32,7 @@ def child(cfg: str, libname: str):
     t.lba_plucker(want_outputs=False)
     kt = t.kernel_times()
     print(json.dumps({"lib": libname, "lba_ms_median": float(np.median(ms[1:])),
+                      "chi2": [float(x) for x in r.get("chi2", [])],
                       "kernels_us": {k: round(1e3 * v[0] / max(v[1], 1), 2) for k, v in kt.items()}}))
 
 
