@@ -1154,6 +1154,13 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
 // trial -> decide -> commit. Every kernel is guarded by the device control block, so a fixed
 // sequence can be captured once and replayed; steps after the schedule finished are no-ops.
 // Sum of n doubles over the ranks of a sharded window: send (this rank's partials) -> recv.
+// Device -> host read on the context's own stream. Never the legacy stream (plain hipMemcpy):
+// while another context of the process captures its step graphs (first batch of a new window),
+// a legacy-stream copy is refused and invalidates that capture.
+hipError_t d2h(plba_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    return e == hipSuccess ? hipStreamSynchronize(ctx->stream) : e;
+}
 int allreduce(plba_ctx *ctx, const double *send, double *recv, size_t n) {
     auto &c = ctx->comm;
     if (n == 0) return PLBA_OK;
@@ -1471,7 +1478,7 @@ int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
     // per-iteration trace written by k_decide
     const int nt = std::min(ctx->h_ctrl->ntrace, kTraceCap);
     std::vector<plba_iter_trace> tr(nt);
-    if (nt) PLBA_CHECK(hipMemcpy(tr.data(), d.trace, sizeof(plba_iter_trace) * nt, hipMemcpyDeviceToHost));
+    if (nt) PLBA_CHECK(d2h(ctx, tr.data(), d.trace, sizeof(plba_iter_trace) * nt));
     ctx->trace.insert(ctx->trace.end(), tr.begin(), tr.end());
     return PLBA_OK;
 }
@@ -1764,7 +1771,7 @@ int plba_download(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_orth
         int rc = gather_outputs(ctx, gv);
         if (rc) return rc;
         if (kf_Tcw && d.n_kf)
-            PLBA_CHECK(hipMemcpy(kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
+            PLBA_CHECK(d2h(ctx, kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12));
         for (int p = 0; p < ctx->n_pt && pt_xyz; ++p)
             for (int k = 0; k < 3; ++k) pt_xyz[3 * p + k] = gv[(size_t)p * 4 + k];
         for (int l = 0; l < ctx->n_ln && ln_orth; ++l)
@@ -1813,7 +1820,7 @@ int plba_lba_plucker(plba_ctx *ctx, plba_result *res) {
             std::vector<double> gv;
             if ((rc = gather_outputs(ctx, gv))) return rc;
             if (res->kf_Tcw && d.n_kf)
-                PLBA_CHECK(hipMemcpy(res->kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToHost));
+                PLBA_CHECK(d2h(ctx, res->kf_Tcw, d.Tb[ctx->cur], sizeof(double) * (size_t)d.n_kf * 12));
             for (int p = 0; p < ctx->n_pt && res->pt_xyz; ++p)
                 for (int k = 0; k < 3; ++k) res->pt_xyz[3 * p + k] = gv[(size_t)p * 4 + k];
             for (int l = 0; l < ctx->n_ln && res->ln_orth; ++l)
@@ -1922,11 +1929,11 @@ int plba_hlm_lba(plba_ctx *ctx, const plba_hlm_state *st, const plba_hlm_params 
     res->dx_norm = std::sqrt(h.dx2);
     res->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (res->kf_x && d.n_kf) {
-        PLBA_CHECK(hipMemcpy(res->kf_x, d.xk[ctx->cur], sizeof(double) * (size_t)d.n_kf * 6, hipMemcpyDeviceToHost));
+        PLBA_CHECK(d2h(ctx, res->kf_x, d.xk[ctx->cur], sizeof(double) * (size_t)d.n_kf * 6));
         // KFs outside kf_list keep the caller's x (the device copy carries them through unchanged)
     }
     if (gba && res->ln_line3d && ctx->n_ln)
-        PLBA_CHECK(hipMemcpy(res->ln_line3d, d.XL[ctx->cur], sizeof(double) * (size_t)ctx->n_ln * 6, hipMemcpyDeviceToHost));
+        PLBA_CHECK(d2h(ctx, res->ln_line3d, d.XL[ctx->cur], sizeof(double) * (size_t)ctx->n_ln * 6));
     return plba_download(ctx, res->kf_Tcw, res->pt_xyz, gba ? nullptr : res->ln_orth);
 }
 
@@ -1959,7 +1966,7 @@ int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *la
 int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [17][8] */) {
 #ifdef PLBA_STAMPS
     if (!ctx || !ctx->d.stamps) return PLBA_E_STATE;
-    PLBA_CHECK(hipMemcpy(out, ctx->d.stamps, 17 * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    PLBA_CHECK(d2h(ctx, out, ctx->d.stamps, 17 * 8 * sizeof(unsigned long long)));
     return PLBA_OK;
 #else
     (void)ctx; (void)out;
@@ -1975,7 +1982,7 @@ int plba_debug_bcr_stamps(plba_ctx *ctx, unsigned long long *out, int32_t cap, i
     const int rows_ = std::max(ctx->d.bcr_N, 1);
     const int n = std::min(cap / kBcrStamps, rows_);
     *rows = rows_;
-    PLBA_CHECK(hipMemcpy(out, ctx->d.bcr_stamps, sizeof(unsigned long long) * (size_t)n * kBcrStamps, hipMemcpyDeviceToHost));
+    PLBA_CHECK(d2h(ctx, out, ctx->d.bcr_stamps, sizeof(unsigned long long) * (size_t)n * kBcrStamps));
     return PLBA_OK;
 }
 
