@@ -152,30 +152,6 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #endif
                 STAMP(0);
                 // B: Gauss–Jordan on block row k across the lanes (pivot lanes 6*sk + p)
-#ifdef PLBA_CL_GJ2
-                // 2x2 pivot blocks (p, p+1): both pivot columns broadcast at once, the block
-                // inverted through its determinant — 10 dependent operations per pivot pair
-                // instead of 14. The zero-pivot test is the scalar one: the first pivot a, the
-                // second d - c·b/a (what the scalar elimination would divide by).
-#pragma unroll
-                for (int p = 0; p < 6; p += 2) {
-                    const int pl = 6 * sk + p;
-                    double f0[6], f1[6];
-#pragma unroll
-                    for (int r = 0; r < 6; ++r) {
-                        f0[r] = readlane_f64(v[r], pl);
-                        f1[r] = readlane_f64(v[r], pl + 1);
-                    }
-                    const double a = f0[p], b = f1[p], c = f0[p + 1], dd = f1[p + 1];
-                    if (a == 0.0 || fma(-c, b * rcp_nr1(a), dd) == 0.0) fail = true;
-                    const double rdet = rcp_nr1(fma(a, dd, -b * c));
-                    const double vp = fma(dd, v[p], -b * v[p + 1]) * rdet;
-                    const double vq = fma(a, v[p + 1], -c * v[p]) * rdet;
-#pragma unroll
-                    for (int r = 0; r < 6; ++r)
-                        v[r] = r == p ? vp : r == p + 1 ? vq : fma(-f1[r], vq, fma(-f0[r], vp, v[r]));
-                }
-#else
 #pragma unroll
                 for (int p = 0; p < 6; ++p) {
                     const int pl = 6 * sk + p;
@@ -192,7 +168,6 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #pragma unroll
                     for (int r = 0; r < 6; ++r) v[r] = r == p ? mp : fma(-f[r], mp, v[r]);
                 }
-#endif
                 STAMP(1);
                 // C: publish X_i = L_{i,k}ᵀ (lane 6s+c holds row c of L_{i,k}) and z_k
                 if (clane && cs != sk) {
