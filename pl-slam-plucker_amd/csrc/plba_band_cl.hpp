@@ -12,7 +12,7 @@
 //   every band block at once, and z_k = S_k⁻¹y_k — no separate S⁻¹ and no separate L product.
 // * The next column k+1 (the next pivot's block column) is formed by the same wave right after
 //   the single workgroup barrier: A_{i,k+1} -= L_{i,k}A_{k+1,k}ᵀ with A_{k+1,k} read from LDS
-//   before the Gauss–Jordan started.
+//   while the X publish and the barrier run.
 // * Worker waves apply step k to the rest of the window (blocks (i,j), k+2 <= j <= i <= k+bw,
 //   and b_i) one step behind, stream block row k+1+bw in, and flush L/z to HBM: they are off
 //   the chain as long as they finish within one Gauss–Jordan.
@@ -143,12 +143,6 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #ifdef PLBA_CL_NOA1  // timing experiment only: wrong results
 #pragma unroll
                 for (int q = 0; q < 36; ++q) a1[q] = 1e-3 * q;
-#else
-#pragma unroll
-                for (int q = 0; q < 36; ++q) a1[q] = pA[s1 * 36 + q];
-                // keep these loads in front of the Gauss–Jordan so their latency hides behind it
-                // (the scheduler would otherwise sink them to their use in E/F)
-                __builtin_amdgcn_sched_barrier(0);
 #endif
                 STAMP(0);
                 // B: Gauss–Jordan on block row k across the lanes (pivot lanes 6*sk + p)
@@ -168,6 +162,14 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #pragma unroll
                     for (int r = 0; r < 6; ++r) v[r] = r == p ? mp : fma(-f[r], mp, v[r]);
                 }
+#ifndef PLBA_CL_NOA1
+                // A_{k+1,k} only feeds E/F: read after the Gauss–Jordan, so B does not wait for
+                // 18 broadcast reads (C and the barrier cover their latency; the sched_barrier
+                // keeps the scheduler from sinking them to their use): step 2,696 -> 2,570 cycles
+#pragma unroll
+                for (int q = 0; q < 36; ++q) a1[q] = pA[s1 * 36 + q];
+                __builtin_amdgcn_sched_barrier(0);
+#endif
                 STAMP(1);
                 // C: publish X_i = L_{i,k}ᵀ (lane 6s+c holds row c of L_{i,k}) and z_k
                 if (clane && cs != sk) {
