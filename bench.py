@@ -243,7 +243,17 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # gloo prints "[Gloo] Rank r is connected to ..." on the process's stdout (fd 1) while
+        # the group forms: send fd 1 to stderr for the init, so stdout carries only the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     from plba.lib import Solver
 
     if a.mode is None:
