@@ -64,7 +64,7 @@ def parse():
                    help="default: replicas (one C3 window per GPU); shard: one C5 window over all ranks")
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="--mode shard all-reduce transport")
     p.add_argument("--no-shard-run", action="store_true", help="replicas, N > 1: skip the embedded sharded C5 run")
-    p.add_argument("--shard-timeout", type=float, default=180.0, help="seconds allowed to the embedded sharded run")
+    p.add_argument("--shard-timeout", type=float, default=90.0, help="seconds allowed to the embedded sharded run")
     p.add_argument("--windows", type=int, default=4,
                    help="N = 1: also time this many independent windows solved concurrently on the one GPU "
                         "(one context + stream each, one host thread each), reported as 'concurrent_windows' "
