@@ -140,7 +140,10 @@ int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on);   /* HIP-event timing 
  * band factorisation (bandwidth <= 9), [14]=super-rows of the block-cyclic-reduction
  * factorisation (0 = not used), [15]=dense RCS on the multi-workgroup MFMA path,
  * [16]=times a block-cyclic-reduction hand-off timed out and the schedule was re-solved with
- * the column-lane factorisation (the context then keeps that factorisation).
+ * the column-lane factorisation (the context then keeps that factorisation), [17]=trial slots
+ * a step evaluates at most (speculative damped trials, 1 = off), [18]=their policy
+ * (0 off, 1 always, 2 after a rejection in the iteration, 3 after the first rejection of the
+ * optimize() call), [19]=device steps the last schedule took.
  * Counts are this rank's when the window is sharded. */
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap);
 int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,

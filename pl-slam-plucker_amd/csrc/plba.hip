@@ -114,6 +114,7 @@ struct plba_ctx {
     hipGraphExec_t multi_exec[kMultiLevels] = {};
     int last_steps = 16;     // steps the previous schedule needed (first batch size)
     int cur = 0;             // which state buffer holds the current estimate (mirror of Ctrl::cur)
+    int last_ok = 0, chi_src = 0;  // x_p / x_l and χ² buffer indices (mirrors of Ctrl::last_ok / chi_src)
     bool no_graph = false;   // set when the step cannot be captured (RCCL without capture support)
     // block cyclic reduction safety net: a BCR hand-off wait that timed out (Ctrl::dev_error)
     // makes run_schedule restore the schedule's starting state from these copies, switch this
@@ -402,6 +403,26 @@ inline bool want_bcr(int bw, int nf, int resident) {
     const double t_cl = 1.3 * (nf + bw) / 2.0, t_bcr = levels * (2.6 * bw + 4.8);
     return t_bcr < t_cl;
 }
+// Trial slots per step and when to use them (DESIGN §2 "Speculative trials"). PLBA_SPEC=<slots>
+// and PLBA_SPEC_POLICY=<0 off | 1 always | 2 after a rejection in the iteration | 3 after the first
+// rejection of the optimize() call> override (A/B runs; results are identical in every setting).
+struct SpecChoice {
+    int slots, policy;
+};
+inline SpecChoice spec_choice(bool cl, bool sharded, bool has_trials, int64_t E) {
+    SpecChoice r{1, kSpecOff};
+    if (!cl || sharded || !has_trials) return r;
+    (void)E;
+    r.slots = 2;
+    r.policy = kSpecSticky;
+    const char *e = getenv("PLBA_SPEC");
+    if (e && e[0]) r.slots = std::max(1, std::min(atoi(e), kMaxSpec));
+    const char *p = getenv("PLBA_SPEC_POLICY");
+    if (p && p[0]) r.policy = std::max(0, std::min(atoi(p), 3));
+    if (r.policy == kSpecOff) r.slots = 1;
+    if (r.slots == 1) r.policy = kSpecOff;
+    return r;
+}
 inline void launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
     if (d.bcr) {  // forward elimination, then back substitution + pose update (plba_bcr.hpp)
@@ -411,7 +432,7 @@ inline void launch_band(Dev &d, hipStream_t s) {
     }
     if (d.cl) {
         const void *k = cl_kernel_impl(d.bw, d.twisted != 0, std::make_integer_sequence<int, kClMaxBW + 1>{});
-        (void)hipLaunchKernel(k, dim3(d.twisted ? 2 : 1), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
+        (void)hipLaunchKernel(k, dim3(d.twisted ? 2 : 1, d.spec_max), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
         return;
     }
     if (d.twisted)
@@ -941,6 +962,17 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.twisted = twisted ? 1 : 0;
     d.tw_m = twisted ? tw_split(nf, bw) : 0;
     d.corrected = ctx->opts.corrected_line_jacobian;
+    // Speculative trials: worth it where the step is bound by the serial factorisation
+    // chain and the rest of the chip idles during it — the column-lane factorisation (one or two
+    // workgroups per trial); the extra slots' edge and landmark kernels are then the price.
+    // Not for BCR (every CU already busy), the dense path or sharded windows (collectives per slot).
+    {
+        const SpecChoice sp = spec_choice(d.cl != 0, sharded, n_lm > 0 && nch > 0, E);
+        d.spec_max = sp.slots;
+        d.spec_policy = sp.policy;
+        d.nbs = d.spec_max + 1;
+        d.nbx = d.spec_max > 1 ? d.spec_max + 1 : 1;
+    }
     {  // timing experiments only (wrong results): PLBA_DIAG bit mask read by some kernels
         const char *dg = getenv("PLBA_DIAG");
         d.diag = dg ? atoi(dg) : 0;
@@ -978,24 +1010,22 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         if (devb) ctx->alloc_dev(p, (size_t)(n_), (dptr)); \
         else UPLOAD(p, v);                                \
     } while (0)
+    const int nbs = d.nbs, nbx = d.nbx, W = d.spec_max;
     UPLOAD(d.T_init, T);
     UPLOAD(d.Tb[0], T);
-    ALLOC(d.Tb[1], T.size());
+    for (int b = 1; b < nbs; ++b) ALLOC(d.Tb[b], T.size());
     UPLOAD_D(d.X_init, X, wb.X, (size_t)n_lm * 4);
     UPLOAD_D(d.Xb[0], X, wb.X, (size_t)n_lm * 4);
-    ALLOC(d.Xb[1], (size_t)n_lm * 4);
-    ALLOC(d.xk[0], (size_t)n_kf * 6);
-    ALLOC(d.xk[1], (size_t)n_kf * 6);
+    for (int b = 1; b < nbs; ++b) ALLOC(d.Xb[b], (size_t)n_lm * 4);
+    for (int b = 0; b < nbs; ++b) ALLOC(d.xk[b], (size_t)n_kf * 6);
     // hand-rolled GBA: endpoint lines in the reference's (global) order, their 6x6 blocks
-    ALLOC(d.XL[0], (size_t)std::max(n_ln_g, 1) * 6);
-    ALLOC(d.XL[1], (size_t)std::max(n_ln_g, 1) * 6);
+    for (int b = 0; b < nbs; ++b) ALLOC(d.XL[b], (size_t)std::max(n_ln_g, 1) * 6);
     ALLOC(d.Hl6, (size_t)std::max(n_ln, 1) * 21);
     ALLOC(d.bl6, (size_t)std::max(n_ln, 1) * 6);
     std::vector<int32_t> ln_gidx(std::max(n_ln, 1), 0);
     for (int i = 0; i < n_ln; ++i) ln_gidx[i] = lm_gpos[n_pt + i] - n_pt_g;
     UPLOAD(d.ln_gidx, ln_gidx);
-    ALLOC(d.Lpb[0], (size_t)std::max(n_ln, 1) * 8);
-    ALLOC(d.Lpb[1], (size_t)std::max(n_ln, 1) * 8);
+    for (int b = 0; b < nbs; ++b) ALLOC(d.Lpb[b], (size_t)std::max(n_ln, 1) * 8);
     UPLOAD(d.kf_hidx, kf_hidx);
     UPLOAD_D(d.e_lm, e_lm, wb.e_lm, E);
     UPLOAD_D(d.e_kf, e_kf, wb.e_kf, E);
@@ -1011,15 +1041,16 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.A, (size_t)E * 12);
     ALLOC(d.cvec, (size_t)E * 2);
     ALLOC(d.B, (size_t)E * 8);
-    ZALLOC(d.chi2_last, E);
+    for (int b = 0; b < nbx; ++b) ZALLOC(d.chi2b[b], E);
     // Hpp | b_p | #active edges | χ² | active | landmark max per rank: one array, all-reduced when sharded
     ALLOC(d.red_iter, (size_t)nf * 43 + 2 + R);
     if (sharded) ALLOC(d.red_iter_loc, (size_t)nf * 43 + 2 + R);
     ALLOC(d.Hll, (size_t)n_lm * 10);
     ALLOC(d.bl, (size_t)n_lm * 4);
-    ALLOC(d.Z, (size_t)E * 8);
-    ALLOC(d.q, (size_t)E * 2);
-    ZALLOC(d.xl, (size_t)n_lm * 4);
+    // λ-dependent arrays: one copy per trial slot, back to back (slot_view, sl_* in plba_kernels.hpp)
+    ALLOC(d.Z, (size_t)W * E * 8);
+    ALLOC(d.q, (size_t)W * E * 2);
+    for (int b = 0; b < nbx; ++b) ZALLOC(d.xlb[b], (size_t)n_lm * 4);
     UPLOAD(d.blk_i1, blk_i1);
     UPLOAD(d.blk_i2, blk_i2);
     UPLOAD(d.blk_off, blk_off);
@@ -1028,24 +1059,25 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     UPLOAD(d.ch_blk, ch_blk);
     UPLOAD(d.ch_off, ch_off);
     UPLOAD(d.blk_ch, blk_ch);
-    ALLOC(d.ch_part, (size_t)std::max(nch, 1) * 42);
+    d.nch = nch;  // (sl_chp)
+    ALLOC(d.ch_part, (size_t)W * sl_chp(d));
     ALLOC(d.Ad, band_mode ? 1 : (size_t)n * n);
     UPLOAD(d.first_blk, first_blk);
     // band blocks outside the envelope (w > i - first_blk[i]) are never assembled and must
     // read as zero: the band kernels sweep all BW block columns of every row
-    ZALLOC(d.Bd, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
-    ALLOC(d.Lband, band_mode ? (size_t)nf * (bw + 1) * 36 : 1);
-    ALLOC(d.Kinv, (size_t)nf * 36);
-    ALLOC(d.zb, (size_t)nf * 6);
+    ZALLOC(d.Bd, (size_t)W * sl_band(d));
+    ALLOC(d.Lband, (size_t)W * sl_band(d));
+    ALLOC(d.Kinv, (size_t)W * nf * 36);
+    ALLOC(d.zb, (size_t)W * nf * 6);
     if (twisted || fb_tw) {
-        ZALLOC(d.Bd2, (size_t)nf * (bw + 1) * 36);
-        ALLOC(d.bs2, (size_t)nf * 6);
-        ALLOC(d.Lband2, (size_t)nf * (bw + 1) * 36);
-        ALLOC(d.Kinv2, (size_t)nf * 36);
-        ALLOC(d.zb2, (size_t)nf * 6);
-        ALLOC(d.tw_sep, 2 * ((size_t)bw * (bw + 1) * 36 + (size_t)bw * 6));
-        ZALLOC(d.tw_fail, 2);
-        ZALLOC(d.tw_count, 1);
+        ZALLOC(d.Bd2, (size_t)W * sl_tw(d));
+        ALLOC(d.bs2, (size_t)W * nf * 6);
+        ALLOC(d.Lband2, (size_t)W * sl_tw(d));
+        ALLOC(d.Kinv2, (size_t)W * nf * 36);
+        ALLOC(d.zb2, (size_t)W * nf * 6);
+        ALLOC(d.tw_sep, (size_t)W * sl_sep(d));
+        ZALLOC(d.tw_fail, 2 * (size_t)W);
+        ZALLOC(d.tw_count, (size_t)W);
     }
     if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate
         ALLOC(d.bcr_pub, (size_t)d.bcr_N * bcr_pub_doubles(bw));
@@ -1066,8 +1098,9 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ctx->alloc(ctx->bk_xl, (size_t)std::max(n_lm, 1) * 4);
     }
     if (!band_mode) ZALLOC(d.bcr_stamps, kBcrStamps);  // dense-path phase stamps (PLBA_DIAG bit 8)
-    ALLOC(d.bs, n);
-    ZALLOC(d.xp, std::max(n, 6));  // k_lm_solve reads x_p[6·max(h, 0) ..] for fixed-pose slots too
+    ALLOC(d.bs, (size_t)W * n);
+    // k_lm_solve reads x_p[6·max(h, 0) ..] for fixed-pose slots too
+    for (int b = 0; b < nbx; ++b) ZALLOC(d.xpb[b], std::max(n, 6));
     ALLOC(d.Wbuf, (size_t)std::max(n, 1) * (kTile + 1));  // W panel + y of the dense path
     UPLOAD(d.tile_first, tile_first);
     UPLOAD(d.tile_last, tile_last);
@@ -1075,17 +1108,18 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.part_any, d.n_lm_blocks);
     ALLOC(d.part_max, nf + d.n_lm_blocks);
     ALLOC(d.pose_part, (size_t)std::max(nf, 1) * kPoseParts * kPP);
-    ALLOC(d.part_lm, std::max(d.n_lms_blocks, 1));
-    ALLOC(d.part_lms, d.n_lms_blocks);
+    ALLOC(d.part_lm, (size_t)W * sl_lms(d));
+    ALLOC(d.part_lms, (size_t)W * sl_lms(d));
     d.fold = sharded ? 0 : 1;
     d.fold_init = d.fold && !getenv("PLBA_NO_FOLD_INIT");
     // arrival counters: lm_solve, iter_reduce (top), RCS blocks, poses, iter_reduce groups
     const int nred = kPoseParts * nf + (d.n_lm > 0 ? d.n_lm_blocks : 0), ngrp = (nred + kRedGrp - 1) / kRedGrp;
     ZALLOC(d.cnt, 2 + (size_t)nblk + nf + ngrp);
+    ZALLOC(d.cnt_rcs, (size_t)W * nblk);  // per trial slot: arrivals per RCS block
     ALLOC(d.wg_red, 3 * (size_t)std::max(nred, 1));
     ALLOC(d.grp_red, 3 * (size_t)std::max(ngrp, 1));
     d.n_ps = std::max(d.n_kf_blocks, d.bcr_N);
-    ZALLOC(d.part_ps, d.n_ps);
+    ZALLOC(d.part_ps, (size_t)W * d.n_ps);
     ZALLOC(d.ctrl, 1);
     ALLOC(d.trace, kTraceCap);
     ALLOC(ctx->d_depth, Ep);
@@ -1115,6 +1149,10 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     mark("host arrays staged");
     int rc = ctx->commit_plan();
     if (rc) return rc;
+    // slot 0's buffers for the kernels that never run speculatively (one χ² / solve buffer then)
+    d.xp = d.xpb[0];
+    d.xl = d.xlb[0];
+    d.chi2_last = d.chi2b[0];
     d.Hpp = d.red_iter;
     d.bp = d.red_iter + (size_t)nf * 36;
     d.pact = d.red_iter + (size_t)nf * 42;
@@ -1146,7 +1184,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     mark("alloc + copy + memset");
     ctx->uploaded = true;
     ctx->initialized = false;
-    ctx->cur = 0;
+    ctx->cur = ctx->last_ok = ctx->chi_src = 0;
     return PLBA_OK;
 }
 
@@ -1216,11 +1254,11 @@ int launch_step(plba_ctx *ctx) {
     if (!(d.fold_init && reduced))  // (folded into the last k_iter_reduce workgroup otherwise)
         LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_init, dim3(1), dim3(kInitNT), 0, s, d));
     if (d.n_lm > 0) {
-        LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
+        LAUNCH(K_ESCHUR, hipLaunchKernelGGL(k_edge_schur, dim3(d.n_lin_blocks, d.spec_max), dim3(kBlock), 0, s, d));
     }
     if (d.n > 0) {
         if (!d.band_mode) LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
-        if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(chunk_direct ? k_rcs_chunk<false> : k_rcs_chunk<true>, dim3(d.nch), dim3(64), 0, s, d));
+        if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(chunk_direct ? k_rcs_chunk<false> : k_rcs_chunk<true>, dim3(8 * ((d.nch + 7) / 8), d.spec_max), dim3(64), 0, s, d));
         if (d.sharded) {
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
             COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);
@@ -1245,7 +1283,7 @@ int launch_step(plba_ctx *ctx) {
     // the factorisation kernels end with the pose update; without free poses it runs alone
     if (d.n == 0 && d.n_kf > 0) LAUNCH(K_POSE_UPDATE, hipLaunchKernelGGL(k_pose_update, dim3(1), dim3(kBlock), 0, s, d));
     if (d.n_lm > 0) {
-        LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lms_blocks), dim3(kLmsNT), 0, s, d));
+        LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lms_blocks, d.spec_max), dim3(kLmsNT), 0, s, d));
     }
     if (d.sharded) {
         LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide_pack, dim3(1), dim3(kBlock), 0, s, d));
@@ -1317,7 +1355,7 @@ int graph_levels() {
 std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
     const Dev &d = ctx->d;
     return {d.E > 0, d.nf > 0, d.n_lm > 0, d.n > 0, d.nch > 0, d.band_mode, d.dense_mfma, d.dense_mfma ? d.ntiles : 0,
-            d.bw, d.bcr, d.cl, d.twisted, d.sharded, d.fold, d.fold_init, d.n_kf > 0,
+            d.bw, d.bcr, d.cl, d.twisted, d.sharded, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
             (int64_t)(getenv("PLBA_CHUNK_DIRECT") != nullptr), (int64_t)ctx->comm.kind};
 }
 int capture_step(plba_ctx *ctx) {
@@ -1475,6 +1513,8 @@ int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
     ctx->steps_launched = launched;
     ctx->last_steps = std::max(4, ctx->h_ctrl->steps + 1);
     ctx->cur = ctx->h_ctrl->cur;
+    ctx->last_ok = ctx->h_ctrl->last_ok;
+    ctx->chi_src = ctx->h_ctrl->chi_src;
     // per-iteration trace written by k_decide
     const int nt = std::min(ctx->h_ctrl->ntrace, kTraceCap);
     std::vector<plba_iter_trace> tr(nt);
@@ -1517,9 +1557,12 @@ Ctrl schedule_init(plba_ctx *ctx, int n_stages) {
     c.stage = -1;
     c.n_stages = n_stages;
     c.switch_pending = 1;
-    c.solve_ok = 1;
+    c.solve_ok[0] = 1;
     c.max_trials = ctx->opts.max_trials;
     c.cur = ctx->cur;
+    c.last_ok = ctx->last_ok;
+    c.chi_src = ctx->chi_src;
+    c.spec_w = 1;
     return c;
 }
 
@@ -1586,7 +1629,7 @@ int download_outputs(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_o
         ctx->h_out_cap = cap;
     }
     hipLaunchKernelGGL(k_out_scatter, dim3(blocks_for(m)), dim3(kBlock), 0, s, d, ctx->d_outd, ept_depth_ok ? 1 : 0,
-                       ctx->cur);
+                       ctx->cur, ctx->chi_src);
     PLBA_CHECK(hipGetLastError());
     PLBA_CHECK(hipMemcpyAsync(ctx->h_out, ctx->d_outd, bytes, hipMemcpyDeviceToHost, s));
     PLBA_CHECK(hipStreamSynchronize(s));
@@ -1679,14 +1722,17 @@ int plba_upload(plba_ctx *ctx, const plba_graph *g) {
 int plba_reset_estimates(plba_ctx *ctx) {
     if (!ctx || !ctx->uploaded) return ctx ? PLBA_E_STATE : PLBA_E_INVALID;
     Dev &d = ctx->d;
-    ctx->cur = 0;
+    ctx->cur = ctx->last_ok = ctx->chi_src = 0;
     PLBA_CHECK(hipMemcpyAsync(d.Tb[0], d.T_init, sizeof(double) * (size_t)d.n_kf * 12, hipMemcpyDeviceToDevice, ctx->stream));
     PLBA_CHECK(hipMemcpyAsync(d.Xb[0], d.X_init, sizeof(double) * (size_t)d.n_lm * 4, hipMemcpyDeviceToDevice, ctx->stream));
     PLBA_CHECK(hipMemsetAsync(&d.ctrl->cur, 0, sizeof(int32_t), ctx->stream));
+    PLBA_CHECK(hipMemsetAsync(&d.ctrl->last_ok, 0, 2 * sizeof(int32_t), ctx->stream));  // last_ok, chi_src
     PLBA_CHECK(hipMemsetAsync(d.e_level, 0, std::max(d.E, 1), ctx->stream));
-    PLBA_CHECK(hipMemsetAsync(d.xp, 0, sizeof(double) * std::max(d.n, 1), ctx->stream));
-    PLBA_CHECK(hipMemsetAsync(d.xl, 0, sizeof(double) * std::max((size_t)d.n_lm * 4, (size_t)1), ctx->stream));
-    PLBA_CHECK(hipMemsetAsync(d.chi2_last, 0, sizeof(double) * std::max(d.E, 1), ctx->stream));
+    for (int b = 0; b < d.nbx; ++b) {
+        PLBA_CHECK(hipMemsetAsync(d.xpb[b], 0, sizeof(double) * std::max(d.n, 1), ctx->stream));
+        PLBA_CHECK(hipMemsetAsync(d.xlb[b], 0, sizeof(double) * std::max((size_t)d.n_lm * 4, (size_t)1), ctx->stream));
+        PLBA_CHECK(hipMemsetAsync(d.chi2b[b], 0, sizeof(double) * std::max(d.E, 1), ctx->stream));
+    }
     std::fill(ctx->h_level.begin(), ctx->h_level.end(), 0);
     ctx->robust = 1;
     ctx->initialized = false;
@@ -1989,11 +2035,12 @@ int plba_debug_bcr_stamps(plba_ctx *ctx, unsigned long long *out, int32_t cap, i
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[17] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+    const int64_t v[20] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
                            ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N,
-                           ctx->d.dense_mfma, ctx->bcr_fallbacks};
-    for (int i = 0; i < cap && i < 17; ++i) out[i] = v[i];
+                           ctx->d.dense_mfma, ctx->bcr_fallbacks, ctx->d.spec_max, ctx->d.spec_policy,
+                           ctx->h_ctrl ? ctx->h_ctrl->steps : 0};
+    for (int i = 0; i < cap && i < 20; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

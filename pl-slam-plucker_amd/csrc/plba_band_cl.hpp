@@ -311,22 +311,23 @@ __device__ __forceinline__ void cl_store_sep(const double *lds, int k1, double *
 }
 
 template <int BW>
-__global__ __launch_bounds__(kClNT) void k_rcs_factor_band_cl(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kClNT) void k_rcs_factor_band_cl(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_fail;
     if constexpr (BW >= 1 && BW <= kClMaxBW) {
         const BandSeg g{d.Bd, d.bs, d.Lband, nullptr, d.zb, d.nf, d.nf, nullptr};
         bool fail = false;
         cl_forward<BW>(g, 0, d.nf, true, lds, fail);
+        if (diag_fail(d)) fail = true;
         if (threadIdx.x == 0) {
             s_fail = fail ? 1 : 0;
-            d.ctrl->solve_ok = fail ? 0 : 1;
+            *d.solve_okp = fail ? 0 : 1;
         }
         __syncthreads();
         if (!s_fail && threadIdx.x < 64) band_backward_rl<BW>(d.Lband, d.zb, d.nf, d.nf, nullptr, d.xp, false, d.nf, threadIdx.x);
         __syncthreads();
-        pose_update_wg<kClNT>(d);  // applied even after a failed solve, with the previous x_p (A13)
+        pose_update_wg<kClNT>(d, s_fail != 0);  // applied even after a failed solve, with the previous x_p (A13)
     }
 }
 
@@ -339,8 +340,8 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_band_cl(Dev d) {
 // is itself a band of width bw), so no dense separator solve is needed. Back substitution: the
 // separator rows first (one wave), then both segments concurrently on two waves.
 template <int BW>
-__global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_fail, s_last;
     if constexpr (BW >= 1 && BW <= kClMaxBW) {
@@ -424,8 +425,8 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d) {
         cl_forward<BW>(g0, m, m + BW, false, lds, fail2);
         CL_MARK(3);
         if (tid == 0) {
-            if (fail2) s_fail = 1;
-            d.ctrl->solve_ok = s_fail ? 0 : 1;
+            if (fail2 || diag_fail(d)) s_fail = 1;
+            *d.solve_okp = s_fail ? 0 : 1;
         }
         __syncthreads();
         if (!s_fail) {
@@ -445,6 +446,6 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d) {
             CL_MARK(5);  // (count: one unit of t1 - t0 ~ 0 is not a count; see stamp_diag.py)
         }
         __syncthreads();
-        pose_update_wg<kClNT>(d);  // applied even after a failed solve, with the previous x_p (A13)
+        pose_update_wg<kClNT>(d, s_fail != 0);  // applied even after a failed solve, with the previous x_p (A13)
     }
 }

@@ -573,7 +573,7 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
             for (int t = tid; t < S * NX; t += NT) Xg[t] = Rm[(t / NX) * RS + t % NX];
         } else {
             for (int r = tid; r < S; r += NT) st_sc1(d.bcr_x + r, Rm[r * RS + 2 * S]);
-            if (tid == 0) d.ctrl->solve_ok = fail_fwd != 0.0 ? 0 : 1;  // every failure word has flowed in
+            if (tid == 0) d.ctrl->solve_ok[0] = fail_fwd != 0.0 ? 0 : 1;  // every failure word has flowed in
             bcr_publish(&d.bcr_flag[1], epoch);
         }
         BCR_STAMP(16);
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d) {
         }
         // ---- this super-row's poses: x_p (kept from the previous trial if the solve failed, A13),
         //      oplus into the trial state, pose part of Σx(λx+b)
-        const bool failed = d.ctrl->solve_ok == 0;
+        const bool failed = d.ctrl->solve_ok[0] == 0;
         const double lam = ps[BW * 24];
         double sc = 0.0;
         if (tid < BW) {

@@ -41,7 +41,7 @@ constexpr int kDensePanelNT = 64;  // one wave: two row tiles per workgroup
 __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
     TRIAL_GUARD
     DENSE_STAMP(0);
-    if (K > 0 && d.ctrl->solve_ok == 0) return;  // an earlier panel hit a zero pivot
+    if (K > 0 && d.ctrl->solve_ok[0] == 0) return;  // an earlier panel hit a zero pivot
     DENSE_STAMP(1);
     const int lane = threadIdx.x, r = lane & 31, n = d.n;
     const int k0 = K * kDT, kb = min(kDT, n - k0);
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(kDensePanelNT) void k_dense_panel(Dev d, int K) {
     for (int p = 0; p < kDT; ++p)
         if (p < r) t[p] = t[p] / D[p];
     if (blockIdx.x == 0) {
-        if (lane == 0 && (K == 0 || !ok)) d.ctrl->solve_ok = ok ? 1 : 0;
+        if (lane == 0 && (K == 0 || !ok)) d.ctrl->solve_ok[0] = ok ? 1 : 0;
         if (ok && lane < 32 && r < kb) {
 #pragma unroll
             for (int c = 0; c < kDT; ++c)
@@ -139,7 +139,7 @@ __device__ __forceinline__ void dense_tile_of(int t, int K, int &I, int &J) {
 __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
     TRIAL_GUARD
     DENSE_STAMP(8);
-    if (d.ctrl->solve_ok == 0) return;
+    if (d.ctrl->solve_ok[0] == 0) return;
     __shared__ double Ws[kDT][kDT + 1];  // W_IK rows
     __shared__ double Ls[kDT][kDT + 1];  // L_JK rows
     const int lane = threadIdx.x, n = d.n;
@@ -222,15 +222,16 @@ __global__ __launch_bounds__(64) void k_dense_update(Dev d, int K) {
 }
 
 // forward / backward substitution through the dense factor + pose update (one workgroup)
-__global__ __launch_bounds__(kFacThreads) void k_dense_solve(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kFacThreads) void k_dense_solve(Dev d0) {
+    TRIAL_SLOT(0)
     SOLVE_STAMP(12);
-    if (d.ctrl->solve_ok) {  // forward substitution done by the panels / updates (dense_yd)
+    const bool ok = *d.solve_okp != 0;
+    if (ok) {  // forward substitution done by the panels / updates (dense_yd)
         if (d.n <= d.solve_lds_n) dense_solve_wg<true, true>(d);
         else dense_solve_wg<false, true>(d);
     }
     __syncthreads();
     SOLVE_STAMP(14);
-    pose_update_wg<kFacThreads>(d);  // applied even after a failed solve, with the previous x_p (A13)
+    pose_update_wg<kFacThreads>(d, !ok);  // applied even after a failed solve, with the previous x_p (A13)
     SOLVE_STAMP(15);
 }

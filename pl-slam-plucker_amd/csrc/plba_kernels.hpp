@@ -49,6 +49,14 @@ constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window 
 #define PLBA_BAND_NT 1024
 #endif
 constexpr int kBandNT = PLBA_BAND_NT; // threads of the banded factorisation workgroup
+// Speculative trials (DESIGN §2 "Speculative trials"): a step may evaluate up to kMaxSpec damped
+// trials of one linearisation at once — λ, λ·ν, λ·ν·2ν, ... (exactly the λ sequence g2o's
+// Levenberg loop walks after rejections) — in trial slots 0..W-1 (blockIdx.y of the trial
+// kernels); k_decide consumes them in order, as the sequential loop would have evaluated them.
+// State-like arrays rotate through kNB buffers so that no slot overwrites the current state,
+// the last consumed χ² or the last successful solve.
+constexpr int kMaxSpec = 4;
+constexpr int kNB = kMaxSpec + 1;
 
 // Device-resident LM control block: the g2o optimize()/solve() loop runs as a state machine
 // advanced by k_decide, so the host only replays a captured "step" graph and polls this block.
@@ -56,7 +64,12 @@ struct Ctrl {
     double lambda, ni, currentChi, tempChi, rho, scale, maxdiag;
     double chi2_start, lambda_start;
     double chi2_final[2];
-    int32_t qmax, accept, solve_ok, broke;
+    int32_t qmax, accept, broke;
+    int32_t solve_ok[kMaxSpec];                        // per trial slot: the factorisation succeeded
+    int32_t last_ok, chi_src;                          // xp/xl buffer of the last successful consumed solve,
+                                                       // χ² buffer of the last consumed trial (or linearisation)
+    int32_t spec_w, spec_sticky;                       // trial slots of the next step; a rejection seen in
+                                                       // this optimize() call
     int32_t stage, n_stages, iter, need_iter;        // schedule position
     int32_t all_done, switch_pending, robust, level;
     int32_t max_iters[2], iters_done[2];
@@ -83,16 +96,28 @@ struct Dev {
     Cam cam;
     double huber_pt, huber_ln, tau;
     // state
-    // state buffers: Tb[ctrl->cur] is the current estimate, Tb[cur^1] the trial; accepting a trial
-    // flips ctrl->cur (g2o's push/pop/discardTop without a copy)
-    double *Tb[2], *T_init;             // [n_kf][12]
-    double *Xb[2], *X_init;             // [n_lm][4]
-    double *xk[2];                      // [n_kf][6] se(3) pose vectors X_i of the hand-rolled LM
-    double *XL[2];                      // [n_ln_g][6] GBA line3D endpoints, reference (global) line order
+    // state buffers: Tb[ctrl->cur] is the current estimate; trial slot s writes Tb[(cur+1+s) % nbs];
+    // accepting slot s moves ctrl->cur there (g2o's push/pop/discardTop without a copy)
+    double *Tb[kNB], *T_init;           // [n_kf][12]
+    double *Xb[kNB], *X_init;           // [n_lm][4]
+    double *xk[kNB];                    // [n_kf][6] se(3) pose vectors X_i of the hand-rolled LM
+    double *XL[kNB];                    // [n_ln_g][6] GBA line3D endpoints, reference (global) line order
     double *Hl6, *bl6;                  // [n_ln][21], [n_ln][6] GBA line blocks (packed lower 6x6)
     int32_t *ln_gidx;                   // [n_ln] device line -> reference (global) line index
-    double *Lpb[2];                     // [n_ln][8]: Plücker vector (6) of each line at Xb[i]
+    double *Lpb[kNB];                   // [n_ln][8]: Plücker vector (6) of each line at Xb[i]
                                         //   (k_line_pluker at schedule start, then k_lm_solve)
+    // solve / χ² buffers: slot s writes xpb/xlb[(last_ok+1+s) % nbx] and chi2b[(chi_src+1+s) % nbx]
+    // (nbx = 1 without speculation: one buffer, as g2o's _x and the edges' _error)
+    double *xpb[kNB], *xlb[kNB], *chi2b[kNB];
+    int32_t nbs, nbx;                   // state buffers (spec_max + 1), solve / χ² buffers
+    int32_t spec_max, spec_policy;      // trial slots captured per step; when to use them (kSpec*)
+    // ---- resolved per trial slot by slot_view() (trial kernels) / cur_view() (others)
+    int32_t slot;
+    double lam;                         // λ of this slot
+    double *Tc, *Tt, *Xc, *Xt, *Lpc, *Lpt, *xkc, *xkt, *XLc, *XLt;  // current / trial state of the slot
+    double *xp_prev, *xl_prev;          // solution of the last successful solve (used when this one fails)
+    int32_t *solve_okp;                 // &ctrl->solve_ok[slot]
+    int32_t *cnt_rcs;                   // [spec_max][nblk] arrival counters of the RCS blocks
     int32_t *kf_hidx;                   // [n_kf]
     // edges, landmark-major CSR order (points first, then lines)
     int32_t *e_lm, *e_kf, *e_hidx;      // [E]
@@ -103,7 +128,7 @@ struct Dev {
     uint8_t *lm_active;                 // [n_lm]
     int32_t *pe_off, *pe_list;          // free-pose-major edge lists [nf+1], [..]
     // linearisation
-    double *A, *cvec, *B, *chi2_last;   // [E][12], [E][2], [E][8], [E]
+    double *A, *cvec, *B, *chi2_last;   // [E][12], [E][2], [E][8], [E] (chi2_last: this slot's χ² buffer)
     double *Hpp, *bp;                   // [nf][36], [nf][6]
     double *Hll, *bl;                   // [n_lm][10], [n_lm][4]
     // Schur
@@ -175,10 +200,76 @@ struct Dev {
 };
 
 
+// current state, read straight from the kernel arguments (kernels outside the trial: the index is
+// dynamic, so these must not be applied to a local copy of Dev)
 __device__ __forceinline__ double *Tcur(const Dev &d) { return d.Tb[d.ctrl->cur]; }
-__device__ __forceinline__ double *Ttrial(const Dev &d) { return d.Tb[d.ctrl->cur ^ 1]; }
 __device__ __forceinline__ double *Xcur(const Dev &d) { return d.Xb[d.ctrl->cur]; }
-__device__ __forceinline__ double *Xtrial(const Dev &d) { return d.Xb[d.ctrl->cur ^ 1]; }
+// per-edge χ² as g2o's edges hold it (the last consumed trial's, or the last linearisation's)
+__device__ __forceinline__ double *chi2cur(const Dev &d) { return d.chi2b[d.ctrl->chi_src]; }
+
+// element counts of the per-slot arrays (each allocated spec_max times back to back; the host
+// allocation in plba.hip uses the same functions)
+__host__ __device__ __forceinline__ size_t sl_band(const Dev &d) { return d.band_mode ? (size_t)d.nf * (d.bw + 1) * 36 : 1; }
+__host__ __device__ __forceinline__ size_t sl_tw(const Dev &d) { return (size_t)d.nf * (d.bw + 1) * 36; }
+__host__ __device__ __forceinline__ size_t sl_sep(const Dev &d) {
+    return 2 * ((size_t)d.bw * (d.bw + 1) * 36 + (size_t)d.bw * 6);
+}
+__host__ __device__ __forceinline__ size_t sl_chp(const Dev &d) { return (size_t)(d.nch > 1 ? d.nch : 1) * 42; }
+__host__ __device__ __forceinline__ size_t sl_lms(const Dev &d) { return (size_t)(d.n_lms_blocks > 1 ? d.n_lms_blocks : 1); }
+
+// The window as trial slot s sees it: λ_s (g2o's λ after s rejections: λ *= ν, ν *= 2 — the same
+// operations in the same order, so bitwise the λ the sequential loop would use), the state it
+// starts from and the buffers it writes, and its own copies of every λ-dependent array.
+// Returns a copy of Dev whose rotating-buffer arrays (Tb, Xb, ...) must not be indexed: only the
+// resolved pointers are valid in it.
+__device__ __forceinline__ Dev slot_view(const Dev &d0, int s) {
+    Dev d = d0;
+    const Ctrl *c = d0.ctrl;
+    double lam = c->lambda, ni = c->ni;
+    for (int k = 0; k < s; ++k) {
+        lam *= ni;
+        ni *= 2.0;
+    }
+    d.slot = s;
+    d.lam = lam;
+    const int cur = c->cur, ts = (cur + 1 + s) % d0.nbs;
+    d.Tc = d0.Tb[cur]; d.Tt = d0.Tb[ts];
+    d.Xc = d0.Xb[cur]; d.Xt = d0.Xb[ts];
+    d.Lpc = d0.Lpb[cur]; d.Lpt = d0.Lpb[ts];
+    d.xkc = d0.xk[cur]; d.xkt = d0.xk[ts];
+    d.XLc = d0.XL[cur]; d.XLt = d0.XL[ts];
+    const int lo = c->last_ok, xw = (lo + 1 + s) % d0.nbx;
+    d.xp = d0.xpb[xw]; d.xl = d0.xlb[xw];
+    d.xp_prev = d0.xpb[lo]; d.xl_prev = d0.xlb[lo];
+    d.chi2_last = d0.chi2b[(c->chi_src + 1 + s) % d0.nbx];
+    d.solve_okp = const_cast<int32_t *>(c->solve_ok) + s;
+    if (s) {
+        const size_t E = (size_t)d0.E, nf = (size_t)d0.nf, ss = (size_t)s;
+        d.Z += ss * E * 8;
+        d.q += ss * E * 2;
+        d.ch_part += ss * sl_chp(d0);
+        d.Bd += ss * sl_band(d0);
+        d.Lband += ss * sl_band(d0);
+        d.bs += ss * (size_t)d0.n;
+        d.Kinv += ss * nf * 36;
+        d.zb += ss * nf * 6;
+        if (d0.twisted) {
+            d.Bd2 += ss * sl_tw(d0);
+            d.Lband2 += ss * sl_tw(d0);
+            d.bs2 += ss * nf * 6;
+            d.Kinv2 += ss * nf * 36;
+            d.zb2 += ss * nf * 6;
+            d.tw_sep += ss * sl_sep(d0);
+            d.tw_fail += 2 * ss;
+            d.tw_count += ss;
+        }
+        d.part_lm += ss * sl_lms(d0);
+        d.part_lms += ss * sl_lms(d0);
+        d.part_ps += ss * (size_t)d0.n_ps;
+        d.cnt_rcs += ss * (size_t)d0.nblk;
+    }
+    return d;
+}
 
 // ---------------------------------------------------------------- block reductions
 __device__ __forceinline__ double wave_sum(double v) {
@@ -282,11 +373,24 @@ __device__ __forceinline__ void lds_barrier() {
     }
 constexpr double kChi2Thr = 5.991;  // src/mapHandler.cpp:6129,6142
 // a stage skipped by k_iter_init (no active edge) leaves switch_pending set: no trial
-#define TRIAL_GUARD                                                          \
+// PLBA_DIAG bit 128 (tests only): the column-lane factorisation reports a failed solve whenever
+// bits 20.. of λ's representation are ≡ 0 (mod 3) — a deterministic function of the trial's λ, so
+// runs with and without speculative slots fail the same trials (exercises A13's failure path).
+__device__ __forceinline__ bool diag_fail(const Dev &d) {
+    return (d.diag & 128) && ((unsigned long long)__double_as_longlong(d.lam) >> 20) % 3 == 0;
+}
+#define TRIAL_GUARD_OF(dd)                                                   \
     {                                                                        \
-        const Ctrl *cg = d.ctrl;                                             \
+        const Ctrl *cg = (dd).ctrl;                                          \
         if (cg->all_done || cg->switch_pending || cg->dev_error) return;     \
     }
+#define TRIAL_GUARD TRIAL_GUARD_OF(d)
+// Trial kernels take the window as d0 and work on slot_view(d0, S): slots at or above this
+// step's width (Ctrl::spec_w) exit at once.
+#define TRIAL_SLOT(S)                                   \
+    TRIAL_GUARD_OF(d0)                                  \
+    if ((int)(S) >= d0.ctrl->spec_w) return;            \
+    const Dev d = slot_view(d0, (int)(S));
 
 __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
     ITER_GUARD
@@ -297,13 +401,19 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
     const bool sw = cc->switch_pending;
     const int nxt = cc->stage + 1;
     const int robust = sw ? cc->stage_robust[nxt] : cc->robust;
+    double *chi2e = chi2cur(d);  // this iteration's χ² go where the last consumed trial's are
     if (e < d.E) {
         double *A = d.A + (size_t)e * 12, *c = d.cvec + (size_t)e * 2, *B = d.B + (size_t)e * 8;
         if (sw) {
+            const double stale = chi2e[e];
+            // every χ² buffer starts the stage with the stale values: an edge the new stage leaves
+            // inactive keeps its χ² whichever buffer the stage's last trial writes
+            for (int b = 0; b < d.nbx; ++b)
+                if (d.chi2b[b] != chi2e) d.chi2b[b][e] = stale;
             // stage switch: classify on the stale χ² and the current depth (src/mapHandler.cpp:
             // 6125-6147), then activate the edges of the optimised level
             if (cc->stage_classify[nxt]) {
-                bool bad = d.chi2_last[e] > kChi2Thr;
+                bool bad = stale > kChi2Thr;
                 if (e < d.Ep) {
                     double Pc[3];
                     point_pc(Tcur(d) + (size_t)d.e_kf[e] * 12, Xcur(d) + (size_t)d.e_lm[e] * 4, Pc);
@@ -342,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
                 for (int k = 0; k < 6; ++k) L[k] = Lc[k];
                 hlm_line(d.T_init + (size_t)kf * 12, L, obs, d.cam, cc->hlm_homog, r, w, Jp, Jl);
             }
-            d.chi2_last[e] = r * r;
+            chi2e[e] = r * r;
             rc = r * r * w;
             const double sw = sqrt(w);
             const bool pose_free = d.e_hidx[e] >= 0;
@@ -389,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
             }
             const double info = d.e_info[e];
             const double chi = err[0] * (info * err[0]) + err[1] * (info * err[1]);
-            d.chi2_last[e] = chi;
+            chi2e[e] = chi;
             double rho0 = chi, rho1 = 1.0;
             if (robust) huber(chi, delta, rho0, rho1);
             rc = rho0;
@@ -836,10 +946,7 @@ __device__ __forceinline__ void rcs_finalize_entry(const Dev &d, int b, int e, d
         // SURVEY.md §8 A13); its all-zero block row becomes I (x = 0 exactly) instead of λI,
         // which would be a zero pivot at λ = 0
         // (hand-rolled LM: Marquardt damping H(i,i) += λ·H(i,i), src/mapHandler.cpp:2114-2115)
-        if (r == c) {
-            const Ctrl *cg = d.ctrl;
-            h += d.pact[i1] == 0.0 ? 1.0 : cg->hlm ? cg->lambda * d.Hpp[(size_t)i1 * 36 + e] : cg->lambda;
-        }
+        if (r == c) h += d.pact[i1] == 0.0 ? 1.0 : d.ctrl->hlm ? d.lam * d.Hpp[(size_t)i1 * 36 + e] : d.lam;
         if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
         else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
         if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1)) * 36 + e] = h;
@@ -861,15 +968,18 @@ __device__ __forceinline__ void rcs_finalize_entry(const Dev &d, int b, int e, d
 // own row. The arithmetic per lane is unchanged (bitwise-identical sums).
 typedef double dbl2 __attribute__((ext_vector_type(2)));  // register-promotable 16-B pair
 template <bool STAGED>
-__global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(64) void k_rcs_chunk(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
     __shared__ double smem[64 * 43];  // staging: A₁ | A₂ (64x12) | Z₁ | Z₂ (64x8); then red[64][43]
     double(*red)[43] = reinterpret_cast<double(*)[43]>(smem);
     // XCD-aware remap (blocks are dealt round-robin over the 8 XCDs): each XCD gets a contiguous
     // run of chunks = a contiguous range of RCS block rows, so the A/Z rows of the landmarks
-    // they couple are re-read from that XCD's L2 instead of the fabric (speed only)
-    const int nb = gridDim.x, per = (nb + 7) / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    // they couple are re-read from that XCD's L2 instead of the fabric (speed only). The grid's x
+    // extent is padded to a multiple of 8 so that every trial slot (blockIdx.y) sees the same
+    // block -> XCD assignment; the padding blocks exit.
+    const int nb = d.nch, per = (nb + 7) / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
     const int full = nb - 8 * (per - 1);  // XCDs that get `per` chunks (the rest get per-1)
+    if (xcd >= full && slot >= per - 1) return;  // padding
     const int ch = xcd < full ? xcd * per + slot : full * per + (xcd - full) * (per - 1) + slot;
     const int lane = threadIdx.x;
     const bool hlm = d.ctrl->hlm != 0;
@@ -992,7 +1102,7 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
         st_sc1(d.ch_part + (size_t)ch * 42 + lane, sacc);
     }
     // the last chunk of block b to arrive assembles the block (the k_rcs_finalize entry work)
-    if (d.fold && arrive_last(d.cnt + 2 + b, d.blk_ch[b + 1] - d.blk_ch[b]) && lane < 42) {
+    if (d.fold && arrive_last(d.cnt_rcs + b, d.blk_ch[b + 1] - d.blk_ch[b]) && lane < 42) {
         double sacc = 0.0;
         const int c1 = d.blk_ch[b + 1];
         for (int c0 = d.blk_ch[b]; c0 < c1; c0 += 4) {  // 4 partials in flight, summed in chunk order
@@ -1007,8 +1117,8 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d) {
 }
 
 // sharded pass 2a: this rank's per-block sums (chunks in order) into the all-reduced array
-__global__ __launch_bounds__(kBlock) void k_rcs_blockpart(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kBlock) void k_rcs_blockpart(Dev d0) {
+    TRIAL_SLOT(0)
     const int gid = blockIdx.x * kBlock + threadIdx.x;
     const int b = gid / 42, e = gid % 42;
     if (b >= d.nblk) return;
@@ -1022,8 +1132,8 @@ __global__ __launch_bounds__(kBlock) void k_rcs_blockpart(Dev d) {
 
 // pass 2: per block entry, sum its chunks in order, add Hpp + λI (diagonal), write the band /
 // dense matrix and b_s = b_p - Σ A_eᵀ q_e.
-__global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d0) {
+    TRIAL_SLOT(0)
     const int gid = blockIdx.x * kBlock + threadIdx.x;
     const int b = gid / 42, e = gid % 42;
     if (b >= d.nblk) return;
@@ -1037,15 +1147,16 @@ __global__ __launch_bounds__(kBlock) void k_rcs_finalize(Dev d) {
 }
 
 // oplus of every free pose with x_p (trial state; fixed poses copied), and the pose part of
-// Σx(λx+b), reduced over the NT threads of one workgroup into part_ps[0] (other slots zeroed)
+// Σx(λx+b), reduced over the NT threads of one workgroup into part_ps[0] (other slots zeroed).
+// `d` is a slot view; `failed`: the solve failed, x_p is the last successful solve's (A13).
 template <int NT>
-__device__ __forceinline__ void pose_update_wg(const Dev &d) {
+__device__ __forceinline__ void pose_update_wg(const Dev &d, bool failed) {
     __shared__ double sh_pu[NT / 64];
     double sc = 0.0;
-    const double lam = d.ctrl->lambda;
-    const int hlm = d.ctrl->hlm, cur = d.ctrl->cur;
-    const double *Tc0 = Tcur(d);
-    double *Tt0 = Ttrial(d);
+    const double lam = d.lam;
+    const int hlm = d.ctrl->hlm;
+    const double *Tc0 = d.Tc, *xp = failed ? d.xp_prev : d.xp;
+    double *Tt0 = d.Tt;
     for (int k = threadIdx.x; k < d.n_kf; k += NT) {
         const double *Tc = Tc0 + (size_t)k * 12;
         double *Tt = Tt0 + (size_t)k * 12;
@@ -1056,17 +1167,17 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
             double x[6], xn[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                x[i] = d.xp[6 * h + i];
+                x[i] = xp[6 * h + i];
                 sc += x[i] * x[i];
             }
-            hlm_pose_update(d.xk[cur] + (size_t)k * 6, x, xn, Tt);
+            hlm_pose_update(d.xkc + (size_t)k * 6, x, xn, Tt);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) d.xk[cur ^ 1][(size_t)k * 6 + i] = xn[i];
+            for (int i = 0; i < 6; ++i) d.xkt[(size_t)k * 6 + i] = xn[i];
         } else if (h >= 0) {
             double x[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                x[i] = d.xp[6 * h + i];
+                x[i] = xp[6 * h + i];
                 sc += x[i] * (lam * x[i] + d.bp[(size_t)h * 6 + i]);
             }
             pose_oplus(Tc, x, Tt);
@@ -1075,7 +1186,7 @@ __device__ __forceinline__ void pose_update_wg(const Dev &d) {
             for (int i = 0; i < 12; ++i) Tt[i] = Tc[i];
             if (hlm)
 #pragma unroll
-                for (int i = 0; i < 6; ++i) d.xk[cur ^ 1][(size_t)k * 6 + i] = d.xk[cur][(size_t)k * 6 + i];
+                for (int i = 0; i < 6; ++i) d.xkt[(size_t)k * 6 + i] = d.xkc[(size_t)k * 6 + i];
         }
     }
     const double s = block_sum<NT>(sc, sh_pu);
@@ -1226,8 +1337,8 @@ __device__ __forceinline__ void dense_solve_wg(const Dev &d) {
 
 // Envelope-aware tiled LDLᵀ of the lower triangle + solve, one workgroup of 1024 threads.
 // Semantics of Eigen::SimplicialLDLT as used by LinearSolverEigen: fails iff a pivot is 0.
-__global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d0) {
+    TRIAL_SLOT(0)
     __shared__ double T[kTile][kTile + 1];
     __shared__ double Dk[kTile];
     __shared__ int s_fail;
@@ -1311,13 +1422,13 @@ __global__ __launch_bounds__(kFacThreads) void k_rcs_factor(Dev d) {
         }
     }
     __syncthreads();
-    if (tid == 0) d.ctrl->solve_ok = s_fail ? 0 : 1;
+    if (tid == 0) *d.solve_okp = s_fail ? 0 : 1;
     if (!s_fail) {  // on failure x_p keeps its previous value (g2o leaves _x untouched)
         if (n <= d.solve_lds_n) dense_solve_wg<true>(d);
         else dense_solve_wg<false>(d);
     }
     __syncthreads();
-    pose_update_wg<kFacThreads>(d);  // the update is applied even after a failed solve (A13)
+    pose_update_wg<kFacThreads>(d, s_fail != 0);  // the update is applied even after a failed solve (A13)
 }
 
 
@@ -1765,12 +1876,12 @@ __device__ __forceinline__ void band_backward(const double *Lband, const double 
 }
 
 template <int BW>
-__global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d0) {
+    TRIAL_SLOT(0)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const BandSeg g{d.Bd, d.bs, d.Lband, d.Kinv, d.zb, d.nf, d.nf, nullptr};
     const bool fail = band_forward<BW>(g, lds, d.ring, d.stamps);
-    if (threadIdx.x == 0) d.ctrl->solve_ok = fail ? 0 : 1;
+    if (threadIdx.x == 0) *d.solve_okp = fail ? 0 : 1;
     if (!fail && threadIdx.x < 64) {
         double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
         band_lds<BW>(lds, d.ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
@@ -1778,7 +1889,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
         else band_backward<BW>(d.Lband, d.zb, d.nf, d.nf, nullptr, d.xp, false, d.nf, xr, part, threadIdx.x);
     }
     __syncthreads();
-    pose_update_wg<kBandNT>(d);  // applied even after a failed solve, with the previous x_p (A13)
+    pose_update_wg<kBandNT>(d, fail);  // applied even after a failed solve, with the previous x_p (A13)
 }
 
 // Two-sided ("twisted") banded LDLᵀ: workgroup 0 eliminates block rows 0..m-1 top-down,
@@ -1789,8 +1900,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d) {
 // (dense Gauss–Jordan, no pivoting: the pivots are LDLᵀ pivots, a zero one fails the solve as
 // SimplicialLDLT does) and runs both back substitutions on two waves. Half the serial chain.
 template <int BW>
-__device__ __forceinline__ void k_rcs_factor_twisted_body(Dev &d) {
-    TRIAL_GUARD
+__device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
     constexpr int W = BW + 1, NT = kBandNT, NS = 6 * BW, LD = NS + 1;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_last, s_sfail;
@@ -1934,13 +2044,16 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(Dev &d) {
     }  // both segments eliminated
 #undef TW_MARK
     __syncthreads();
-    if (tid == 0) d.ctrl->solve_ok = s_sfail ? 0 : 1;
-    pose_update_wg<NT>(d);  // applied even after a failed solve, with the previous x_p (A13)
+    if (tid == 0) *d.solve_okp = s_sfail ? 0 : 1;
+    pose_update_wg<NT>(d, s_sfail != 0);  // applied even after a failed solve, with the previous x_p (A13)
 }
 
 template <int BW>
-__global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d) {
-    if constexpr (BW >= 1) k_rcs_factor_twisted_body<BW>(d);  // (the host never selects bw 0)
+__global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d0) {
+    if constexpr (BW >= 1) {  // (the host never selects bw 0)
+        TRIAL_SLOT(0)
+        k_rcs_factor_twisted_body<BW>(d);
+    }
 }
 
 #include "plba_band_cl.hpp"
@@ -1950,9 +2063,9 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d) {
 
 // ---------------------------------------------------------------- update + trial evaluation
 // stand-alone pose update (windows without free poses: no factorisation kernel to fuse into)
-__global__ __launch_bounds__(kBlock) void k_pose_update(Dev d) {
-    TRIAL_GUARD
-    if (blockIdx.x == 0) pose_update_wg<kBlock>(d);
+__global__ __launch_bounds__(kBlock) void k_pose_update(Dev d0) {
+    TRIAL_SLOT(0)
+    if (blockIdx.x == 0) pose_update_wg<kBlock>(d, false);
 }
 
 // ---------------------------------------------------------------- edge-parallel trial path
@@ -1995,13 +2108,13 @@ __device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, bool mu
     }
 }
 // per edge: Z_e = B_e L⁻ᵀ (rows solved with L), q_e = Z_e g
-__global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
     const int e = blockIdx.x * kBlock + threadIdx.x;
     if (e >= d.E) return;
     const int l = d.e_lm[e];
     if (e >= d.Ep && d.ctrl->hlm == 2) {  // GBA line: 6x6 (Hl6 + λ·diag) = L Lᵀ, Z_e = L⁻¹ b_e, q_e = Z_e·L⁻¹ b_l
-        const double lam = d.ctrl->lambda;
+        const double lam = d.lam;
         const int li = l - d.n_pt;
         double H[21], L6[21], g6[6], bb[6], z[6];
 #pragma unroll
@@ -2046,7 +2159,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d) {
     }
     const int DIM = e < d.Ep ? 3 : 4;
     double L[10], g[4], B[8];
-    lm_chol(d, l, d.ctrl->lambda, d.ctrl->hlm != 0, L, g);
+    lm_chol(d, l, d.lam, d.ctrl->hlm != 0, L, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) B[k] = d.B[(size_t)e * 8 + k];
     double z[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -2207,43 +2320,61 @@ __device__ __forceinline__ double lm_eval(const Dev &d, const LmEdge &s, const d
 // OptimizationAlgorithmLevenberg trial decision + optimize() loop control.
 // Runs as its own launch (sharded windows, windows without landmarks) or as the tail of the last
 // k_lm_solve workgroup; the landmark partials are read with sc1 loads in both cases.
+// Speculative steps: the W = Ctrl::spec_w trial slots evaluated λ_0 = λ, λ_1 = λ·ν, ... of the
+// same linearisation from the same state; they are consumed in slot order exactly as g2o's loop
+// would have met them (slot s is only reached when slot s-1 was rejected and the loop goes on,
+// and then λ, ν here equal the λ_s, ν_s slot s used, bit for bit), and the slots after an
+// accepted or iteration-ending trial are discarded. A failed solve (zero pivot) uses the last
+// successful solve's x; a slot whose solve failed after an earlier slot of the same step had
+// succeeded saw the wrong "last" x, so it is not consumed: the next step evaluates it again,
+// alone (one slot: no concurrent writer of the buffers it reads).
+constexpr int kSpecOff = 0, kSpecAlways = 1, kSpecAfterReject = 2, kSpecSticky = 3;
 template <int NT>
 __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
-    double a = 0.0, b = 0.0;
-    if (!d.sharded) {  // 8 loads of each array in flight per thread; summed in index order
-        constexpr int U = 8;
-        for (int i0 = threadIdx.x; i0 < d.n_lms_blocks; i0 += NT * U) {
-            double va[U], vb[U];
+    const int W = d.ctrl->spec_w;  // trial slots this step evaluated (uniform)
+    double tch[kMaxSpec], scl[kMaxSpec];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * NT;
-                const bool ok = i < d.n_lms_blocks;
-                va[u] = ok ? ld_sc1(d.part_lm + i) : 0.0;
-                vb[u] = ok ? ld_sc1(d.part_lms + i) : 0.0;
-            }
+    for (int s = 0; s < kMaxSpec; ++s) {
+        tch[s] = scl[s] = 0.0;
+        if (s >= W) continue;
+        const double *plm = d.part_lm + (size_t)s * sl_lms(d), *plms = d.part_lms + (size_t)s * sl_lms(d);
+        const double *pps = d.part_ps + (size_t)s * d.n_ps;
+        double a = 0.0, b = 0.0;
+        if (!d.sharded) {  // 8 loads of each array in flight per thread; summed in index order
+            constexpr int U = 8;
+            for (int i0 = threadIdx.x; i0 < d.n_lms_blocks; i0 += NT * U) {
+                double va[U], vb[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                a += va[u];
-                b += vb[u];
+                for (int u = 0; u < U; ++u) {
+                    const int i = i0 + u * NT;
+                    const bool ok = i < d.n_lms_blocks;
+                    va[u] = ok ? ld_sc1(plm + i) : 0.0;
+                    vb[u] = ok ? ld_sc1(plms + i) : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    a += va[u];
+                    b += vb[u];
+                }
             }
         }
+        for (int i = threadIdx.x; i < d.n_ps; i += NT) b += pps[i];  // poses: replicated
+        tch[s] = block_sum<NT>(a, sh);
+        scl[s] = block_sum<NT>(b, sh);
     }
-    for (int i = threadIdx.x; i < d.n_ps; i += NT) b += d.part_ps[i];  // poses: replicated
-    double tempChi0 = block_sum<NT>(a, sh);
-    double scale0 = block_sum<NT>(b, sh);
-    if (d.sharded) {  // landmark terms summed over ranks
-        tempChi0 = d.red_dec[0];
-        scale0 += d.red_dec[1];
+    if (d.sharded) {  // landmark terms summed over ranks (one slot)
+        tch[0] = d.red_dec[0];
+        scl[0] += d.red_dec[1];
     }
     if (threadIdx.x != 0) return;
     Ctrl *c = d.ctrl;
     c->steps += 1;
-    if (c->hlm) {  // src/mapHandler.cpp:1867-1895 (first step), :2121-2156
+    if (c->hlm) {  // src/mapHandler.cpp:1867-1895 (first step), :2121-2156 — one slot
         const double lam0 = c->lambda;
         const bool first = c->iter == 0;
         int result = 0;
         c->hlm_solves += 1;
-        c->dx2 = scale0;
+        c->dx2 = scl[0];
         bool apply;
         if (first) {
             apply = true;
@@ -2255,9 +2386,11 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
             c->lambda *= c->hlm_k;
             apply = true;
         }
-        apply = apply && c->solve_ok;  // (an LDLᵀ breakdown leaves X unchanged)
+        const bool ok = c->solve_ok[0] != 0;
+        if (ok) c->last_ok = (c->last_ok + 1) % d.nbx;
+        apply = apply && ok;  // (an LDLᵀ breakdown leaves X unchanged)
         if (apply) {
-            c->cur ^= 1;
+            c->cur = (c->cur + 1) % d.nbs;
             c->hlm_acc += 1;
         }
         if (c->ntrace < kTraceCap)
@@ -2265,7 +2398,7 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
                                                    c->lambda};
         c->iters_done[c->stage] += 1;
         c->iter += 1;
-        const bool small = !first && sqrt(scale0) < c->hlm_minchg;
+        const bool small = !first && sqrt(scl[0]) < c->hlm_minchg;
         c->err_prev = c->currentChi;
         if (small || c->iter >= c->max_iters[c->stage]) {
             c->chi2_final[c->stage] = c->currentChi;
@@ -2273,48 +2406,82 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
         } else {
             c->need_iter = 1;
         }
+        c->spec_w = 1;
         return;
     }
-    double tempChi = tempChi0;
-    if (!c->solve_ok) tempChi = 1.7976931348623157e308;
-    const double scale = scale0 + 1e-3;
-    const double rho = (c->currentChi - tempChi) / scale;
-    c->tempChi = tempChi;
-    c->scale = scale;
-    c->rho = rho;
-    if (rho > 0 && isfinite(tempChi)) {
-        double alpha = 1. - pow((2 * rho - 1), 3);
-        alpha = fmin(alpha, 2. / 3.);
-        const double sf = fmax(1. / 3., alpha);
-        c->lambda *= sf;
-        c->ni = 2;
-        c->currentChi = tempChi;
-        c->accept = 1;
-        c->qmax += 1;
-    } else {
-        c->lambda *= c->ni;
-        c->ni *= 2;
-        c->accept = 0;
-        if (!isfinite(c->lambda)) c->broke = 1;
-        else c->qmax += 1;
+    const int cur0 = c->cur, lo0 = c->last_ok, ch0 = c->chi_src;
+    bool any_ok = false, hold = false, trials_go_on = false, done = false;
+#pragma unroll
+    for (int s = 0; s < kMaxSpec; ++s) {
+        if (done || s >= W) continue;
+        const bool ok = c->solve_ok[s] != 0;
+        if (!ok && any_ok) {  // evaluated with the wrong "last successful" x: evaluate again alone
+            hold = true;
+            done = true;
+            continue;
+        }
+        c->chi_src = (ch0 + 1 + s) % d.nbx;  // the edges now hold this trial's χ² (stale if rejected)
+        if (ok) {
+            c->last_ok = (lo0 + 1 + s) % d.nbx;
+            any_ok = true;
+        }
+        double tempChi = tch[s];
+        if (!ok) tempChi = 1.7976931348623157e308;
+        const double scale = scl[s] + 1e-3;
+        const double rho = (c->currentChi - tempChi) / scale;
+        c->tempChi = tempChi;
+        c->scale = scale;
+        c->rho = rho;
+        if (rho > 0 && isfinite(tempChi)) {
+            double alpha = 1. - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2. / 3.);
+            const double sf = fmax(1. / 3., alpha);
+            c->lambda *= sf;
+            c->ni = 2;
+            c->currentChi = tempChi;
+            c->accept = 1;
+            c->qmax += 1;
+            c->cur = (cur0 + 1 + s) % d.nbs;  // the trial becomes the current estimate
+        } else {
+            c->lambda *= c->ni;
+            c->ni *= 2;
+            c->accept = 0;
+            c->spec_sticky = 1;
+            if (!isfinite(c->lambda)) c->broke = 1;
+            else c->qmax += 1;
+        }
+        const bool again = !c->broke && rho < 0 && c->qmax < c->max_trials;
+        if (again) {  // another damped trial of this iteration: the next slot, or the next step
+            trials_go_on = true;
+            continue;
+        }
+        trials_go_on = false;
+        done = true;
+        // end of OptimizationAlgorithmLevenberg::solve(iter)
+        const int terminate = (c->qmax == c->max_trials || rho == 0 || !isfinite(c->lambda)) ? 1 : 0;
+        if (c->ntrace < kTraceCap)
+            d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, c->qmax, terminate, c->chi2_start, c->currentChi,
+                                                   c->lambda_start, c->lambda};
+        c->iters_done[c->stage] += 1;
+        c->iter += 1;
+        if (terminate || c->iter >= c->max_iters[c->stage]) {  // optimize() returns
+            c->chi2_final[c->stage] = c->currentChi;
+            c->spec_sticky = 0;
+            if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
+            else c->all_done = 1;
+        } else {
+            c->need_iter = 1;
+        }
     }
-    if (c->accept) c->cur ^= 1;  // the trial becomes the current estimate
-    const bool again = !c->broke && rho < 0 && c->qmax < c->max_trials;
-    if (again) return;  // another damped trial of this iteration
-    // end of OptimizationAlgorithmLevenberg::solve(iter)
-    const int terminate = (c->qmax == c->max_trials || rho == 0 || !isfinite(c->lambda)) ? 1 : 0;
-    if (c->ntrace < kTraceCap)
-        d.trace[c->ntrace++] = plba_iter_trace{c->stage, c->iter, c->qmax, terminate, c->chi2_start, c->currentChi,
-                                               c->lambda_start, c->lambda};
-    c->iters_done[c->stage] += 1;
-    c->iter += 1;
-    if (terminate || c->iter >= c->max_iters[c->stage]) {  // optimize() returns
-        c->chi2_final[c->stage] = c->currentChi;
-        if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
-        else c->all_done = 1;
-    } else {
-        c->need_iter = 1;
+    // the next step's trial slots (Dev::spec_policy)
+    int w = 1;
+    if (d.spec_max > 1 && !hold) {
+        const int pol = d.spec_policy;
+        if (pol == kSpecAlways) w = d.spec_max;
+        else if (pol == kSpecAfterReject) w = trials_go_on ? d.spec_max : 1;
+        else if (pol == kSpecSticky) w = c->spec_sticky ? d.spec_max : 1;
     }
+    c->spec_w = w;
 }
 __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
     TRIAL_GUARD
@@ -2322,25 +2489,25 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
     decide_body<kBlock>(d, sh);
 }
 
-__global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
     __shared__ double sh[kLmsNT / 64];
+    const int nslots = d0.ctrl->spec_w;  // (read before this workgroup arrives: k_decide changes it)
     const int gt = blockIdx.x * kLmsNT + threadIdx.x;
     const int l = gt / kLmLanes, q = gt % kLmLanes;   // a quad never straddles a wave
     const bool live = l < d.n_lm;
     const int lc = live ? l : 0;
     const Ctrl *cg = d.ctrl;
-    const bool solve = cg->solve_ok != 0;
+    const bool solve = *d.solve_okp != 0;
     const bool robust = cg->robust != 0;
-    const double lam = cg->lambda;
-    const int cur = cg->cur;
+    const double lam = d.lam;
     const bool hlm = cg->hlm != 0;
     // ---- round 1: landmark record + this lane's edge slots
     const bool act = live && d.lm_active[lc] != 0;
     const int off0 = d.lm_off[lc], off1 = d.lm_off[lc + 1];
     double Xc[4], bl[4], H[10];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) Xc[k] = d.Xb[cur][(size_t)lc * 4 + k];
+    for (int k = 0; k < 4; ++k) Xc[k] = d.Xc[(size_t)lc * 4 + k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) bl[k] = d.bl[(size_t)lc * 4 + k];
 #pragma unroll
@@ -2354,7 +2521,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
         lm_load_edge(d, sv[j] ? e : 0, sl[j]);
     }
     // ---- round 2: x_p of each slot's free pose, the slot's trial pose
-    const double *Tt0 = d.Tb[cur ^ 1];
+    const double *Tt0 = d.Tt;
     double xs[kLmSlots][6], Ts[kLmSlots][12];
 #pragma unroll
     for (int j = 0; j < kLmSlots; ++j) {
@@ -2399,9 +2566,9 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
         // GBA line (src/mapHandler.cpp:3673-3691): x = (Hl6 + λ·diag)⁻¹ (b_l − Σ_e b_e a_e·x_p),
         // X += DX on the 6 endpoint coordinates, ‖DX‖² partial; lane q == 0 writes
         const int li = l - d.n_pt, j = d.ln_gidx[li];
-        const double *XLc = d.XL[cur] + (size_t)j * 6;
-        double *XLt = d.XL[cur ^ 1] + (size_t)j * 6;
-        double *Xt = d.Xb[cur ^ 1] + (size_t)l * 4;
+        const double *XLc = d.XLc + (size_t)j * 6;
+        double *XLt = d.XLt + (size_t)j * 6;
+        double *Xt = d.Xt + (size_t)l * 4;
         if (act && solve) {
             double H[21], L6[21], y[6], x[6];
 #pragma unroll
@@ -2451,7 +2618,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
     } else if (live) {
-        double *Xt = d.Xb[cur ^ 1] + (size_t)l * 4;
+        double *Xt = d.Xt + (size_t)l * 4;
         if (act) {
             const bool pt = is_point_lm(d, l);
             const int DIM = pt ? 3 : 4;
@@ -2500,9 +2667,9 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) d.xl[(size_t)l * 4 + i] = x[i];
                 }
-            } else {
+            } else {  // failed solve: the last successful solve's x (A13)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) x[i] = d.xl[(size_t)l * 4 + i];
+                for (int i = 0; i < 4; ++i) x[i] = d.xl_prev[(size_t)l * 4 + i];
             }
             if (q == 0) {
 #pragma unroll
@@ -2519,7 +2686,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
             } else if (!(d.diag & 1)) {
                 Xt[q] = orth_oplus_quad(Xc, x, q, Lp);
                 if (q == 0) {
-                    double *Lt = d.Lpb[cur ^ 1] + (size_t)(l - d.n_pt) * 8;
+                    double *Lt = d.Lpt + (size_t)(l - d.n_pt) * 8;
 #pragma unroll
                     for (int k = 0; k < 6; ++k) Lt[k] = Lp[k];
                 }
@@ -2542,8 +2709,8 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) Xt[i] = Xc[i];
                 if (!is_point_lm(d, l)) {  // an inactive line keeps its Plücker vector too
-                    const double *Lc = d.Lpb[cur] + (size_t)(l - d.n_pt) * 8;
-                    double *Lt = d.Lpb[cur ^ 1] + (size_t)(l - d.n_pt) * 8;
+                    const double *Lc = d.Lpc + (size_t)(l - d.n_pt) * 8;
+                    double *Lt = d.Lpt + (size_t)(l - d.n_pt) * 8;
 #pragma unroll
                     for (int k = 0; k < 6; ++k) Lt[k] = Lc[k];
                 }
@@ -2557,7 +2724,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d) {
         st_sc1(d.part_lm + blockIdx.x, s1);
     }
     // the last workgroup to finish takes the trial decision (k_decide's work)
-    if (d.fold && arrive_last(d.cnt, (int32_t)gridDim.x)) decide_body<kLmsNT>(d, sh);
+    if (d.fold && arrive_last(d.cnt, (int32_t)gridDim.x * nslots)) decide_body<kLmsNT>(d0, sh);
 }
 // sharded: this rank's trial χ² and landmark scale terms into the all-reduced decision array
 __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
@@ -2605,7 +2772,7 @@ __global__ void k_refresh(Dev d, int level) {
         line_error(T, L, obs, d.cam, err);
     }
     const double info = d.e_info[e];
-    d.chi2_last[e] = err[0] * (info * err[0]) + err[1] * (info * err[1]);
+    chi2cur(d)[e] = err[0] * (info * err[0]) + err[1] * (info * err[1]);
 }
 // isDepthPositive() at the current state
 __global__ void k_depth(Dev d, uint8_t *out) {
@@ -2619,9 +2786,9 @@ __global__ void k_depth(Dev d, uint8_t *out) {
 // unsharded download: poses, landmark states and per-edge outputs in the caller's order, one
 // staging block (Tcw | pt_xyz | ln_orth | χ² by e_gpos, points then lines | bytes:
 // isDepthPositive [Ep] | levels by e_gpos)
-__global__ void k_out_scatter(Dev d, double *od, int want_depth, int cur) {
+__global__ void k_out_scatter(Dev d, double *od, int want_depth, int cur, int chi) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const double *T = d.Tb[cur], *X = d.Xb[cur];  // the host's current state index
+    const double *T = d.Tb[cur], *X = d.Xb[cur];  // the host's current state / χ² buffer index
     const size_t nk = d.n_kf, np = d.n_pt, nl = d.n_ln, E = d.E;
     if (i < d.n_kf)
 #pragma unroll
@@ -2641,7 +2808,7 @@ __global__ void k_out_scatter(Dev d, double *od, int want_depth, int cur) {
     }
     if (i < d.E) {
         const int g = d.e_gpos[i];
-        opt[np * 3 + nl * 4 + g] = d.chi2_last[i];
+        opt[np * 3 + nl * 4 + g] = d.chi2b[chi][i];
         uint8_t *ob = reinterpret_cast<uint8_t *>(opt + np * 3 + nl * 4 + E);
         ob[(size_t)d.Ep + g] = d.e_level[i];
         if (want_depth && i < d.Ep) {
@@ -2662,7 +2829,7 @@ __global__ void k_gather(Dev d, const uint8_t *depth) {
     if (i < d.E) {
         double *o = d.gat + (size_t)d.n_lm_g * 4;
         const int g = d.e_gpos[i];
-        o[g] = d.chi2_last[i];
+        o[g] = chi2cur(d)[i];
         o[(size_t)d.E_g + g] = i < d.Ep ? (double)depth[i] : 0.0;
         o[2 * (size_t)d.E_g + g] = (double)d.e_level[i];
     }

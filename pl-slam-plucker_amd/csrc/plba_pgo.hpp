@@ -340,11 +340,11 @@ __global__ __launch_bounds__(256) void k_pgo_check(Dev d) {
     }
     if (bad) s_bad = 1;  // (benign race: every writer stores 1)
     __syncthreads();
-    if (threadIdx.x == 0 && s_bad) d.ctrl->solve_ok = 0;
+    if (threadIdx.x == 0 && s_bad) d.ctrl->solve_ok[0] = 0;
 }
 
 __global__ __launch_bounds__(kFacThreads) void k_pgo_solve(Dev d) {
-    if (!d.ctrl->solve_ok) return;  // x keeps its previous value (g2o's _x)
+    if (!d.ctrl->solve_ok[0]) return;  // x keeps its previous value (g2o's _x)
     if (d.n <= d.solve_lds_n) dense_solve_wg<true, true>(d);  // forward part done in the factorisation
     else dense_solve_wg<false, true>(d);
 }
@@ -377,7 +377,7 @@ __global__ void k_pgo_sum(PgoDev p, const Ctrl *ctrl, int slot, double lambda) {
         double s = 0.0;
         for (int k = 0; k < p.n; ++k) s += p.x[k] * (lambda * p.x[k] + p.b[k]);
         p.out[2] = s;
-        p.out[3] = ctrl->solve_ok ? 1.0 : 0.0;
+        p.out[3] = ctrl->solve_ok[0] ? 1.0 : 0.0;
     }
 }
 

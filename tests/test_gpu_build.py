@@ -117,3 +117,23 @@ def test_step_graph_update_across_windows(monkeypatch, cfg):
         _, fresh = _solve(monkeypatch, g, host=False)
         for k in KEYS:
             assert np.array_equal(o[k], fresh[k]), k
+
+
+def test_step_graph_update_across_window_sizes(monkeypatch):
+    """Windows of different keyframe counts with the same launch signature (same bandwidth and
+    factorisation): the updated executable graphs carry the new grids and the new dynamic LDS size
+    of the column-lane factorisation (its x_p staging grows with nf) — each solve equals a fresh
+    context's, bitwise (the update path with a changed LDS size / grid)."""
+    from plba.lib import Solver
+    gs = [synth.generate("C2", n_kf=nk, n_pt=100 * nk, n_ln=20 * nk, seed=2000 + nk) for nk in (40, 56, 75)]
+    with Solver() as s:
+        outs, sts = [], []
+        for g in gs:
+            s.upload(g)
+            outs.append(s.lba_plucker())
+            sts.append(s.structure_stats())
+    assert len({st["nf"] for st in sts}) == 3, sts
+    for g, o in zip(gs, outs):
+        _, fresh = _solve(monkeypatch, g, host=False)
+        for k in KEYS:
+            assert np.array_equal(o[k], fresh[k]), k
