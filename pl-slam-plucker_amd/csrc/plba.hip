@@ -121,7 +121,7 @@ struct plba_ctx {
     // context to the column-lane factorisation for good (no_bcr) and solve the window again
     bool no_bcr = false;
     int bcr_fallbacks = 0;
-    int fb_twisted = 0, fb_tw_m = 0;  // the column-lane variant the window falls back to
+    int fb_cl = 0, fb_twisted = 0, fb_tw_m = 0;  // the factorisation the window falls back to
     double *bk_T = nullptr, *bk_X = nullptr, *bk_xp = nullptr, *bk_xk = nullptr, *bk_Lpb = nullptr, *bk_XL = nullptr,
            *bk_xl = nullptr;
     uint8_t *bk_level = nullptr;
@@ -188,12 +188,14 @@ struct plba_ctx {
         for (auto &it : plan)
             if (!it.src && !it.dsrc) { it.off = tot; tot = al(tot + it.bytes); }
         if (tot > arena_cap) {
-            (void)hipStreamSynchronize(stream);
-            if (arena) (void)hipFree(arena);
+            // stream-ordered: hipFree / hipMalloc would synchronise the whole device, which fails
+            // (and invalidates the capture) while another context of the process captures its
+            // step graphs
+            if (arena) (void)hipFreeAsync(arena, stream);
             arena = nullptr;
             arena_cap = 0;
             const size_t cap = tot + tot / 4;
-            if (hipMalloc((void **)&arena, cap) != hipSuccess) {
+            if (hipMallocAsync((void **)&arena, cap, stream) != hipSuccess) {
                 (void)hipGetLastError();
                 set_error("hipMalloc(%zu bytes) of the window arena failed", cap);
                 return PLBA_E_NOMEM;
@@ -202,7 +204,7 @@ struct plba_ctx {
         }
         if (up > staging_cap) {
             (void)hipStreamSynchronize(stream);
-            if (staging) (void)hipHostFree(staging);
+            retire_pinned(staging);
             staging = nullptr;
             staging_cap = 0;
             const size_t cap = up + up / 4;
@@ -224,7 +226,11 @@ struct plba_ctx {
         // reads of memory no kernel wrote; arrays whose zero start is part of the contract stay 0
         const char *poison = getenv("PLBA_POISON");
         const bool pz = poison && poison[0] == '1';
-        hipError_t e = hipMemsetAsync(arena + dv, pz ? 0xFF : 0, tot - dv, stream);
+        // device-sourced arrays [up, dv) are zeroed too before their payload is copied in, so the
+        // padding past their payload reads as zero like a host array's (the 128-byte over-read
+        // contract of alloc) — one memset of [up, tot) unless the rest is poisoned
+        hipError_t e = pz ? hipMemsetAsync(arena + up, 0, dv - up, stream) : hipSuccess;
+        if (e == hipSuccess) e = pz ? hipMemsetAsync(arena + dv, 0xFF, tot - dv, stream) : hipMemsetAsync(arena + up, 0, tot - up, stream);
         for (auto &it : plan)
             if (it.dsrc && it.src_bytes && e == hipSuccess)
                 e = hipMemcpyAsync(arena + it.off, it.dsrc, it.src_bytes, hipMemcpyDeviceToDevice, stream);
@@ -239,6 +245,12 @@ struct plba_ctx {
             return PLBA_E_DEVICE;
         }
         return PLBA_OK;
+    }
+    // Pinned host blocks outgrown by a bigger window are freed only when the context is destroyed:
+    // hipHostFree synchronises the device (see commit_plan). Growth is geometric, so few retire.
+    std::vector<void *> retired;
+    void retire_pinned(void *p) {
+        if (p) retired.push_back(p);
     }
     hipEvent_t next_event() {
         if (ev_next == ev_pool.size()) {
@@ -423,22 +435,21 @@ inline SpecChoice spec_choice(bool cl, bool sharded, bool has_trials, int64_t E)
     if (r.slots == 1) r.policy = kSpecOff;
     return r;
 }
-inline void launch_band(Dev &d, hipStream_t s) {
+// the banded factorisation's launch(es); the first failing launch's status is returned
+inline hipError_t launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
     if (d.bcr) {  // forward elimination, then back substitution + pose update (plba_bcr.hpp)
-        (void)hipLaunchKernel(bcr_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrNT), args, bcr_lds_bytes(d.bw), s);
-        (void)hipLaunchKernel(bcr_back_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrBackNT), args, bcr_back_lds_bytes(d.bw), s);
-        return;
+        hipError_t e = hipLaunchKernel(bcr_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrNT), args, bcr_lds_bytes(d.bw), s);
+        if (e != hipSuccess) return e;
+        return hipLaunchKernel(bcr_back_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrBackNT), args, bcr_back_lds_bytes(d.bw), s);
     }
     if (d.cl) {
         const void *k = cl_kernel_impl(d.bw, d.twisted != 0, std::make_integer_sequence<int, kClMaxBW + 1>{});
-        (void)hipLaunchKernel(k, dim3(d.twisted ? 2 : 1, d.spec_max), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
-        return;
+        return hipLaunchKernel(k, dim3(d.twisted ? 2 : 1, d.spec_max), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
     }
     if (d.twisted)
-        (void)hipLaunchKernel(twisted_kernel(d.bw), dim3(2), dim3(kBandNT), args, twisted_lds_bytes(d.bw, d.nf), s);
-    else
-        (void)hipLaunchKernel(band_kernel(d.bw), dim3(1), dim3(kBandNT), args, band_lds_bytes(d.bw, d.nf), s);
+        return hipLaunchKernel(twisted_kernel(d.bw), dim3(2), dim3(kBandNT), args, twisted_lds_bytes(d.bw, d.nf), s);
+    return hipLaunchKernel(band_kernel(d.bw), dim3(1), dim3(kBandNT), args, band_lds_bytes(d.bw, d.nf), s);
 }
 
 // time a launch when kernel timing is enabled
@@ -954,8 +965,12 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
                          (cl ? cl_lds_bytes(bw, nf, true) : twisted_lds_bytes(bw, nf)) <= 159 * 1024 &&
                          !(no_twist && no_twist[0] == '1');
     // the column-lane factorisation a BCR window falls back to (run_schedule) and its arrays
-    const bool fb_tw = bcr && use_cl(bw) && nf >= 2 * bw + 16 && cl_lds_bytes(bw, nf, true) <= 159 * 1024 &&
+    // (the same checks as the normal column-lane choice; without it, the one-sweep band kernel)
+    static_assert(kBcrMaxBW <= kClMaxBW, "a BCR window must be able to fall back to the column-lane kernel");
+    const bool fb_cl = bcr && use_cl(bw) && cl_lds_bytes(bw, nf, false) <= 159 * 1024;
+    const bool fb_tw = fb_cl && nf >= 2 * bw + 16 && cl_lds_bytes(bw, nf, true) <= 159 * 1024 &&
                        !(no_twist && no_twist[0] == '1');
+    ctx->fb_cl = fb_cl ? 1 : 0;
     ctx->fb_twisted = fb_tw ? 1 : 0;
     ctx->fb_tw_m = fb_tw ? tw_split(nf, bw) : 0;
     d.cl = cl && cl_lds_bytes(bw, nf, twisted) <= 159 * 1024 ? 1 : 0;
@@ -1212,7 +1227,8 @@ int allreduce(plba_ctx *ctx, const double *send, double *recv, size_t n) {
     }
     if (c.kind == plba_ctx::Comm::HOST) {
         if (c.hcap < n) {
-            if (c.hbuf) (void)hipHostFree(c.hbuf);
+            PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+            ctx->retire_pinned(c.hbuf);
             c.hbuf = nullptr;
             PLBA_CHECK(hipHostMalloc((void **)&c.hbuf, n * sizeof(double), hipHostMallocDefault));
             c.hcap = n;
@@ -1267,7 +1283,13 @@ int launch_step(plba_ctx *ctx) {
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
         const size_t solve_lds = d.n <= d.solve_lds_n ? sizeof(double) * (size_t)d.n : 0;  // y of dense_solve_wg
         if (d.band_mode) {
-            LAUNCH(K_FACTOR, launch_band(d, s));
+            hipError_t fe = hipSuccess;
+            LAUNCH(K_FACTOR, fe = launch_band(d, s));
+            if (fe != hipSuccess) {
+                (void)hipGetLastError();
+                ctx->set_error("factorisation launch failed: %s", hipGetErrorString(fe));
+                return PLBA_E_DEVICE;
+            }
         } else if (d.dense_mfma) {  // blocked LDLᵀ, MFMA trailing updates (plba_dense.hpp)
             for (int K = 0; K < d.ntiles; ++K) {  // the envelope's row tiles K..tile_last[K] only
                 const int m = ctx->h_tile_last[K] - K;
@@ -1542,7 +1564,7 @@ int run_schedule(plba_ctx *ctx, const Ctrl &init) {
     destroy_graphs(ctx);
     d.bcr = 0;
     d.bcr_N = 0;
-    d.cl = 1;
+    d.cl = ctx->fb_cl;
     d.twisted = ctx->fb_twisted;
     d.tw_m = ctx->fb_tw_m;
     ctx->no_bcr = true;
@@ -1621,7 +1643,8 @@ int download_outputs(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_o
     const bool any = kf_Tcw || pt_xyz || ln_orth || ept_chi2 || ept_depth_ok || eln_chi2 || ept_level || eln_level;
     if (!m || !any) return PLBA_OK;
     if (bytes > ctx->h_out_cap) {  // grow-only, with slack: the next windows of a session are similar
-        if (ctx->h_out) (void)hipHostFree(ctx->h_out);
+        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->retire_pinned(ctx->h_out);
         ctx->h_out = nullptr;
         ctx->h_out_cap = 0;
         const size_t cap = bytes + bytes / 2;
@@ -1693,13 +1716,16 @@ int plba_destroy(plba_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->free_all();
     destroy_graphs(ctx);
-    if (ctx->arena) (void)hipFree(ctx->arena);
+    if (ctx->arena) (void)hipFreeAsync(ctx->arena, ctx->stream);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->staging) (void)hipHostFree(ctx->staging);
+    for (void *p : ctx->retired) (void)hipHostFree(p);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
-    if (ctx->pgo_mem) (void)hipFree(ctx->pgo_mem);
-    ctx->bmemA.release();
-    ctx->bmemB.release();
+    if (ctx->pgo_mem) (void)hipFreeAsync(ctx->pgo_mem, ctx->stream);
+    ctx->bmemA.release(ctx->stream);
+    ctx->bmemB.release(ctx->stream);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->pgo_hout) (void)hipHostFree(ctx->pgo_hout);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
     if (ctx->comm.hbuf) (void)hipHostFree(ctx->comm.hbuf);
@@ -2362,11 +2388,10 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
     size_t tot = 0;
     for (auto &sl : slots) tot += (std::max(sl.bytes, (size_t)128) + 255) & ~(size_t)255;
     if (tot > ctx->pgo_cap) {
-        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
-        if (ctx->pgo_mem) (void)hipFree(ctx->pgo_mem);
+        if (ctx->pgo_mem) (void)hipFreeAsync(ctx->pgo_mem, ctx->stream);  // stream-ordered (see commit_plan)
         ctx->pgo_mem = nullptr;
         ctx->pgo_cap = 0;
-        if (hipMalloc((void **)&ctx->pgo_mem, tot) != hipSuccess) {
+        if (hipMallocAsync((void **)&ctx->pgo_mem, tot, ctx->stream) != hipSuccess) {
             (void)hipGetLastError();
             ctx->set_error("pose graph: cannot allocate %zu bytes", tot);
             return PLBA_E_NOMEM;

@@ -303,17 +303,18 @@ hipError_t h2d(T *dst, const T *src, size_t n, hipStream_t s) {
 
 }  // namespace
 
-void BuildMem::release() {
-    if (base) (void)hipFree(base);
+// Stream-ordered (hipMallocAsync / hipFreeAsync on the solver stream): a device-synchronising
+// hipFree would fail while another context of the process captures its step graphs.
+void BuildMem::release(hipStream_t s) {
+    if (base) (void)hipFreeAsync(base, s);
     base = nullptr;
     cap = 0;
 }
 int BuildMem::reserve(size_t bytes, hipStream_t s) {
     if (bytes <= cap) return PLBA_OK;
-    (void)hipStreamSynchronize(s);
-    release();
+    release(s);
     const size_t want = bytes + bytes / 4;
-    if (hipMalloc((void **)&base, want) != hipSuccess) {
+    if (hipMallocAsync((void **)&base, want, s) != hipSuccess) {
         (void)hipGetLastError();
         base = nullptr;
         return PLBA_E_NOMEM;

@@ -27,7 +27,7 @@ namespace plba {
 struct BuildMem {
     char *base = nullptr;
     size_t cap = 0;
-    void release();
+    void release(hipStream_t s);
     int reserve(size_t bytes, hipStream_t s);
 };
 

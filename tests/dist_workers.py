@@ -81,12 +81,20 @@ def plan_and_schur_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def sharded_gpu_worker(rank, world, port, outdir, cfg, transport):
-    """GPU rank (all ranks may share one GPU with the host transport): full sharded LBA."""
+def sharded_gpu_worker(rank, world, port, outdir, cfg, transport, host_build=False):
+    """GPU rank (all ranks may share one GPU with the host transport): full sharded LBA.
+    host_build: PLBA_HOST_BUILD=1 (the host window build and its shard_plan) instead of the device
+    build's own ownership kernel (k_b_owner)."""
+    if host_build:
+        os.environ["PLBA_HOST_BUILD"] = "1"
     dist = init_gloo(rank, world, port)
     from plba import synth
     from plba.dist import sharded_solver
+    from plba.lib import shard_plan
     g = synth.generate(cfg)
+    po, lo = shard_plan(g, world)  # the documented plan (plba_shard_plan)
+    plan_lm = int((po == rank).sum() + (lo == rank).sum())
+    plan_e = int((po[g.ept_lm] == rank).sum() + (lo[g.eln_lm] == rank).sum())
     s = sharded_solver(device=0, transport=transport)
     s.upload(g)
     out = s.lba_plucker()
@@ -98,6 +106,7 @@ def sharded_gpu_worker(rank, world, port, outdir, cfg, transport):
              trace_chi2=np.array([t["chi2_end"] for t in out["trace"]]),
              rerun_equal=np.array(all(np.array_equal(out[k], out2[k]) for k in ("kf_Tcw", "pt_xyz", "ln_orth"))),
              local_landmarks=np.array(st["landmarks"]), local_edges=np.array(st["edges"]),
+             plan_landmarks=np.array(plan_lm), plan_edges=np.array(plan_e),
              bcr_fallbacks=np.array(st["bcr_fallbacks"]))
     s.close()
     dist.barrier()

@@ -77,3 +77,49 @@ def test_readback_calls_equal_scattered_outputs():
     np.testing.assert_array_equal(pd, full["ept_depth_ok"])
     np.testing.assert_array_equal(lc, full["eln_chi2"])
     assert_parity(compare(full, ref))
+
+
+def test_concurrent_windows_of_different_sizes_regrow_while_capturing():
+    """contexts that GROW (arena, window-build scratch, pinned download
+    block) while another context of the process captures its step graphs. Three host threads,
+    each a sequence of windows of increasing size (C1L -> C2 -> C3, C2 -> C3, C1L -> C2 -> C4) on its
+    own context, started together: every solve equals the sequential solve of the same window on a
+    fresh context, bitwise (arena / scratch growth is stream-ordered: hipMallocAsync / hipFreeAsync,
+    no device-synchronising call that a concurrent capture would refuse)."""
+    from plba.lib import Solver
+    seqs = [["C1L", "C2", "C3"], ["C2", "C3"], ["C1L", "C2", "C4"]]
+    gs = [[synth.generate(c, seed=synth.CONFIGS[c][3] + 31 * t) for c in seq] for t, seq in enumerate(seqs)]
+    ref = []
+    for row in gs:
+        r = []
+        for g in row:
+            with Solver() as s:
+                s.upload(g)
+                r.append(s.lba_plucker(with_trace=False))
+        ref.append(r)
+    solvers = [Solver() for _ in seqs]
+    outs = [[None] * len(row) for row in gs]
+    errs = []
+    go = threading.Barrier(len(seqs))
+
+    def run(t):
+        try:
+            go.wait()
+            for i, g in enumerate(gs[t]):
+                solvers[t].upload(g)  # grows the context's arena while the others capture / solve
+                outs[t][i] = solvers[t].lba_plucker(with_trace=False)
+        except Exception as e:  # surfaced below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(len(seqs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    for s in solvers:
+        s.close()
+    assert not errs, errs
+    for t in range(len(seqs)):
+        for o, r in zip(outs[t], ref[t]):
+            for k in KEYS:
+                assert np.array_equal(o[k], r[k]), (t, k)

@@ -39,7 +39,29 @@ def test_two_ranks_host_transport_match_oracle(tmp_path, cfg):
     for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2", "ept_level", "iters", "trace_chi2"):
         assert np.array_equal(r[0][k], r[1][k]), k
     assert bool(r[0]["rerun_equal"]) and bool(r[1]["rerun_equal"])
+    # the device build's ownership is plba_shard_plan's: same landmarks and edges per rank
+    for x in r:
+        assert int(x["local_landmarks"]) == int(x["plan_landmarks"]), (int(x["local_landmarks"]), int(x["plan_landmarks"]))
+        assert int(x["local_edges"]) == int(x["plan_edges"]), (int(x["local_edges"]), int(x["plan_edges"]))
     _check(r[0], oa.lba_plucker(g))
+
+
+def test_two_ranks_device_build_equals_host_build(tmp_path):
+    """The sharded device window build (k_b_owner + the device sorts) against the host build with
+    plba_shard_plan on two ranks: every output bitwise equal."""
+    import torch.multiprocessing as mp
+    world = 2
+    res = {}
+    for host in (False, True):
+        d = tmp_path / ("host" if host else "dev")
+        d.mkdir()
+        mp.spawn(dw.sharded_gpu_worker, args=(world, dw.free_port(), str(d), "C2", "host", host), nprocs=world,
+                 join=True)
+        res[host] = [dict(np.load(d / f"rank{i}.npz")) for i in range(world)]
+    for i in range(world):
+        for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2", "ept_level", "iters", "trace_chi2",
+                  "local_landmarks", "local_edges"):
+            assert np.array_equal(res[False][i][k], res[True][i][k]), (i, k)
 
 
 def test_two_ranks_bcr_timeout_fall_back_together(tmp_path, monkeypatch):
@@ -74,6 +96,8 @@ def test_four_ranks_host_transport_match_oracle(tmp_path, cfg):
         for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2", "ept_level", "iters", "trace_chi2"):
             assert np.array_equal(r[0][k], r[i][k]), (i, k)
     assert all(bool(x["rerun_equal"]) for x in r)
+    for x in r:
+        assert int(x["local_landmarks"]) == int(x["plan_landmarks"]) and int(x["local_edges"]) == int(x["plan_edges"])
     _check(r[0], oa.lba_plucker(g))
 
 
