@@ -65,6 +65,7 @@ def parse():
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="--mode shard all-reduce transport")
     p.add_argument("--no-shard-run", action="store_true", help="replicas, N > 1: skip the embedded sharded C5 run")
     p.add_argument("--shard-timeout", type=float, default=90.0, help="seconds allowed to the embedded sharded run")
+    p.add_argument("--no-host-mirror", action="store_true", help="N = 1: skip the host-mirror per-call timing")
     p.add_argument("--windows", type=int, default=4,
                    help="N = 1: also time this many independent windows solved concurrently on the one GPU "
                         "(one context + stream each, one host thread each), reported as 'concurrent_windows' "
@@ -174,6 +175,33 @@ def concurrent_windows(a, dev: int, k: int):
             "ms_per_lba": dt / steps * 1e3,
             "note": "independent windows of the same config, one context + stream + host thread each, "
                     "solved concurrently on one GPU (serving view; not the headline)"}
+
+
+def host_mirror(cfg: str, dev: int, calls: int = 3):
+    """The drop-in's whole per-call cost on the host mirror: the C++
+    MapHandler::localBundleAdjustmentForPlukerWithG2O (src/mapHandler.cpp:5851-6323) on a synthetic
+    map holding the config's window — gather + graph marshalling (:5868-6117), the device solve
+    (upload + two-stage LM + download), the outlier pass (:6154-6293) and the write-back
+    (:6296-6319). Successive calls run on the same map, which each call mutates as the reference's
+    does (outliers removed, fixed observers left local); the first call also creates the context."""
+    from plba.slam_map import HostMap, make_map
+    g = synth.generate(cfg)
+    hm = HostMap(make_map(g), device=dev)
+    rows = []
+    try:
+        for _ in range(calls + 1):
+            rows.append(hm.local_ba())
+    finally:
+        hm.close()
+    warm = rows[1:]
+    med = {k: statistics.median(r[k] for r in warm) for k in ("gather_ms", "solve_ms", "bookkeeping_ms")}
+    return {"gather_ms": med["gather_ms"], "solve_ms": med["solve_ms"], "outlier_and_writeback_ms": med["bookkeeping_ms"],
+            "total_ms": sum(med.values()), "first_call_ms": rows[0]["gather_ms"] + rows[0]["solve_ms"] + rows[0]["bookkeeping_ms"],
+            "calls": calls, "window": {k: rows[-1][k] for k in ("n_free_kf", "n_fixed_kf", "n_pt", "n_ln", "n_ept", "n_eln")},
+            "note": "median of calls 2..%d of MapHandler::localBundleAdjustmentForPlukerWithG2O (host/map_handler.cpp) "
+                    "on one synthetic map: gather = window gather + g2o-graph marshalling, solve = plba_upload + "
+                    "plba_lba_plucker incl. outputs (PCIe-inclusive), outlier_and_writeback = the outlier pass + "
+                    "pose/landmark write-back" % (calls + 1)}
 
 
 def relaunch_distributed(a) -> int:
@@ -368,6 +396,13 @@ def main():
                            "speedup_of_this_run": (tot_iters / dt) / (ri / rdt)}
         dist.barrier()
 
+    hmirror = None
+    if world == 1 and not shard and not a.no_host_mirror:
+        try:
+            hmirror = host_mirror(a.config, dev)
+        except Exception as e:  # informational: must never hide the single-window number
+            hmirror = {"error": repr(e)}
+
     conc = None
     if world == 1 and not shard and a.windows > 1:
         try:
@@ -391,11 +426,25 @@ def main():
         if name == "k_rcs_factor" and info.get("banded"):
             if info.get("bcr_rows"):
                 prof_name = "k_rcs_factor_bcr"
+            elif info.get("quad"):
+                prof_name = "k_rcs_factor_quad_cl"
             else:
                 prof_name = "k_rcs_factor_twisted" if info.get("twisted") else "k_rcs_factor_band"
                 if info.get("column_lane"):
                     prof_name += "_cl"
         alg = kernel_bytes(g, prof_name if prof_name == "k_rcs_factor_bcr" else name, info)
+        # block pivot steps on the factorisation's critical path (forward chain + backward chain)
+        chain = None
+        if name == "k_rcs_factor" and info.get("banded") and not info.get("bcr_rows"):
+            nf_, bw_ = int(info["nf"]), int(info["bw"])
+            if info.get("quad"):
+                L4 = nf_ - 3 * bw_
+                seg = max((L4 + 3) // 4, (L4 - (L4 + 3) // 4 + 1) // 2)
+                chain = 2 * (seg + 2 * bw_)
+            elif info.get("twisted"):
+                chain = 2 * ((nf_ - bw_ + 1) // 2 + bw_)
+            else:
+                chain = 2 * nf_
         achieved = alg / (avg_ms * 1e-3) / 1e9
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
         traffic = None
@@ -405,13 +454,19 @@ def main():
             except Exception:
                 traffic = None
         per_kernel = {}
+        # the iteration kernels exit at once on steps without a new linearisation (ITER_GUARD): their
+        # bandwidth is over the launches that worked — one per outer iteration of the LBA
+        lin_per_lba = int(sum(max(int(x), 0) for x in r["iters"]))
         for k, (ms_k, n_k) in ktimes.items():
             if n_k <= 0:
                 continue
             b = kernel_bytes(g, "k_rcs_factor_bcr" if (k == "k_rcs_factor" and info.get("bcr_rows")) else k, info)
             us = ms_k / n_k * 1e3
-            per_kernel[k] = {"us_per_launch": round(us, 2), "launches_per_lba": n_k,
-                             "alg_bytes": int(b), "GBs": round(b / (us * 1e-6) / 1e9, 1) if b else None}
+            work = min(n_k, lin_per_lba) if k in ("k_linearize", "k_iter_reduce") else n_k
+            us_w = ms_k / max(work, 1) * 1e3
+            per_kernel[k] = {"us_per_launch": round(us, 2), "launches_per_lba": n_k, "working_launches": work,
+                             "us_per_working_launch": round(us_w, 2),
+                             "alg_bytes": int(b), "GBs": round(b / (us_w * 1e-6) / 1e9, 1) if b else None}
         it_per_lba = tot_iters / max(a.steps * (1 if shard else world), 1)
         iter_bytes = synth.algorithmic_bytes_per_iter(g)
         out = {
@@ -438,13 +493,18 @@ def main():
                 "upload_ms": upload_ms,
                 "end_to_end": e2e[-1],
                 "factorisation": ("block cyclic reduction over %d super-rows" % info["bcr_rows"] if info.get("bcr_rows")
-                                  else ("two-sided column-lane band LDLT" if info.get("twisted") else "band LDLT")),
+                                  else ("four-segment column-lane band LDLT" if info.get("quad")
+                                        else ("two-sided column-lane band LDLT" if info.get("twisted") else "band LDLT"))),
+                "speculative_trials": {"slots": info.get("spec_slots", 1), "policy": info.get("spec_policy", 0),
+                                       "device_steps_per_lba": info.get("device_steps")},
                 "parallelism": (f"landmark-sharded window over {world} GPU(s)" if shard
                                 else f"{world} independent windows (1 per GPU)"),
             },
             "roofline": {
                 "kernel": prof_name,
-                "bound": "hbm",
+                # the factorisation is a serial chain of block pivots: its limiter is latency, the HBM
+                # fraction is reported per the contract (peak = HBM) but is not its bound
+                "bound": "latency" if name == "k_rcs_factor" else "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -453,6 +513,8 @@ def main():
                 "alg_bytes_per_launch": alg,
                 "avg_launch_us": avg_ms * 1e3,
                 "launches_per_lba": nl,
+                "critical_path_block_steps": chain,
+                "us_per_block_step": avg_ms * 1e3 / chain if chain else None,
                 "note": ("latency-bound factorisation of the reduced camera system (a serial chain of 6x6 "
                          "pivot blocks or of dense super-row eliminations) + back substitution + pose update; "
                          "bytes/launch are tiny by nature — see DESIGN.md §4"),
@@ -469,8 +531,14 @@ def main():
             out["scaling_reference"] = scaling_ref
         if shard_run is not None:
             out["shard_run"] = shard_run
+            # first-class: the one-window sharded rate (configs[4]) and its speed-up over the same
+            # window unsharded on one GPU, beside the replicas value
+            out["shard_value"] = shard_run.get("value")
+            out["shard_speedup"] = (shard_run.get("scaling_reference") or {}).get("speedup_of_this_run")
         if conc is not None:
             out["concurrent_windows"] = conc
+        if hmirror is not None:
+            out["host_mirror"] = hmirror
         if world == 1 and not a.no_cpu_baseline:
             try:
                 cb = cpu_baseline(a.config, a.cpu_runs if a.config in ("C1", "C1L", "C2", "C3") else 1)

@@ -86,11 +86,13 @@ def test_speculative_slots_are_bitwise_the_sequential_solve(cfg):
         assert_parity(compare(base, oa.lba_plucker(g)))
 
 
-def test_speculative_failed_solves_follow_the_sequential_loop():
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_speculative_failed_solves_follow_the_sequential_loop(cfg):
     """Solves forced to fail by a deterministic function of λ (PLBA_DIAG bit 128): a failed trial is
     rejected and applies the last successful solve's x (A13); a slot failing after an earlier
-    slot of the same step succeeded is evaluated again alone. Bitwise the one-slot run."""
-    g = synth.generate("C2")
+    slot of the same step succeeded is evaluated again alone. Bitwise the one-slot run (C2: the
+    two-sided factorisation, C3: the four-segment one)."""
+    g = synth.generate(cfg)
     base, _, _ = _solve(g, 1, 0, diag=128)
     assert any(t["trials"] > 1 for t in base["trace"]), base["trace"]
     for slots, pol in SETTINGS:

@@ -7,7 +7,7 @@ TAG=${1:-r02}; CFG=${2:-C3}; ST=${3:-10}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
-B="python3 bench.py --config $CFG --steps $ST --warmup 2 --no-cpu-baseline --windows 0"
+B="python3 bench.py --config $CFG --steps $ST --warmup 2 --no-cpu-baseline --windows 0 --no-host-mirror"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- $B > $OUT/bench_trace.json
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o bench --output-format csv -- $B > $OUT/bench_fetch.json
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o bench --output-format csv -- $B > $OUT/bench_write.json
