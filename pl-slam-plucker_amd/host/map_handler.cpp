@@ -183,6 +183,15 @@ Vec6 MapLine::changeOrthToPluker(const Vec4 &o) {
 }
 
 // ----------------------------------------------------------------------------- Window
+void Window::clear() {
+    nofix_kfs.clear(); fix_kfs.clear(); local_pt.clear(); local_ls.clear();
+    max_kf_id = maxPointId = 0;
+    kf_Tcw.clear(); pt_xyz.clear(); ln_orth.clear(); ept_obs.clear(); ept_info.clear(); eln_obs.clear(); eln_info.clear();
+    kf_fixed.clear();
+    kf_id.clear(); pt_id.clear(); ln_id.clear(); ept_lm.clear(); ept_kf.clear(); eln_lm.clear(); eln_kf.clear();
+    ept_kfp.clear(); eln_kfp.clear(); ept_obs_idx.clear(); eln_obs_idx.clear();
+}
+
 plba_graph Window::graph(double fx, double fy, double cx, double cy) const {
     plba_graph g{};
     g.n_kf = (int32_t)kf_id.size();
@@ -227,41 +236,103 @@ void MapHandler::setError(const char *fmt, ...) {
     err_ = buf;
 }
 
-// A1 + A1b: window gather (src/mapHandler.cpp:5868-5921) and graph marshalling (:5923-6117).
-int MapHandler::gatherWindow(Window &w) {
-    w = Window{};
-    // validate every observation first (the reference exit(0)s mid-gather, :5891-5895, 5907-5911)
-    auto valid_kf = [&](int o) {
-        return o >= 0 && o < (int)map_keyframes.size() && map_keyframes[o] && map_keyframes[o]->kf_idx == o;
-    };
-    for (auto *p : map_points)
-        if (p && p->local)
-            for (int o : p->kf_obs_list)
-                if (!valid_kf(o)) {
-                    setError("[Wrong index in the map_keyframes and MapPoint obs] point %d obs kf %d", p->idx, o);
-                    return PLBA_E_INVALID;
-                }
-    for (auto *l : map_lines)
-        if (l && l->local)
-            for (int o : l->kf_obs_list)
-                if (!valid_kf(o)) {
-                    setError("[Wrong index in the map_keyframes and MapLine obs] line %d obs kf %d", l->idx, o);
-                    return PLBA_E_INVALID;
-                }
+static bool has_duplicate_id(const Window &w);
 
-    std::map<int, KeyFrame *> idx_fix_kfs, idx_nofix_kfs, idx_all_kfs;
+// A1 + A1b: window gather (src/mapHandler.cpp:5868-5921) and graph marshalling (:5923-6117).
+// Same sets, orders, ids and error behaviour as the reference's std::map-keyed gather, in one
+// pass over the observations: the per-edge arrays are written with observer ids while the ids
+// are validated and the observers marked; the map is mutated (fixed observers become local) only
+// once every observation is known valid, and the ids are then remapped to kf positions.
+int MapHandler::gatherWindow(Window &w) {
+    w.clear();
+    const int nkf_map = (int)map_keyframes.size();
+    std::vector<uint8_t> valid(nkf_map, 0);
+    for (int o = 0; o < nkf_map; ++o) valid[o] = map_keyframes[o] && map_keyframes[o]->kf_idx == o;
+    std::vector<size_t> pt_off(1, 0), ln_off(1, 0);  // edge offsets per local landmark
+    for (auto *p : map_points)
+        if (p && p->local) {
+            w.local_pt.push_back(p);  // :5877-5881
+            pt_off.push_back(pt_off.back() + p->kf_obs_list.size());
+        }
+    for (auto *l : map_lines)
+        if (l && l->local) {
+            w.local_ls.push_back(l);  // :5882-5886
+            ln_off.push_back(ln_off.back() + l->kf_obs_list.size());
+        }
+    const size_t npt = w.local_pt.size(), nln = w.local_ls.size(), n_ept = pt_off.back(), n_eln = ln_off.back();
+    w.pt_id.resize(npt);
+    w.pt_xyz.resize(npt * 3);
+    w.ept_lm.resize(n_ept);
+    w.ept_kf.resize(n_ept);
+    w.ept_obs.resize(n_ept * 2);
+    w.ept_info.resize(n_ept);
+    w.ept_obs_idx.resize(n_ept);
+    w.ln_id.resize(nln);
+    w.ln_orth.resize(nln * 4);
+    w.eln_lm.resize(n_eln);
+    w.eln_kf.resize(n_eln);
+    w.eln_obs.resize(n_eln * 4);
+    w.eln_info.resize(n_eln);
+    w.eln_obs_idx.resize(n_eln);
+    // The landmark passes read the map only: an invalid observation ends the gather before the
+    // map is touched (the reference exit(0)s, :5891-5895, 5907-5911).
+    std::vector<uint8_t> observer(nkf_map, 0);
+    // point vertices + edges (:5976-6027); ept_kf holds the observer id until the remap below
+    for (size_t li = 0, e = 0; li < npt; ++li) {
+        MapPoint *p = w.local_pt[li];
+        w.pt_id[li] = p->idx;  // + max_kf_id + 1 below
+        for (int k = 0; k < 3; ++k) w.pt_xyz[li * 3 + k] = p->point3D[k];
+        const size_t no = p->kf_obs_list.size();
+        for (size_t i = 0; i < no; ++i, ++e) {
+            const int kf_id = p->kf_obs_list[i];
+            if (kf_id < 0 || kf_id >= nkf_map || !valid[kf_id]) {
+                setError("[Wrong index in the map_keyframes and MapPoint obs] point %d obs kf %d", p->idx, kf_id);
+                w.clear();
+                return PLBA_E_INVALID;
+            }
+            observer[kf_id] = 1;
+            w.ept_lm[e] = (int32_t)li;
+            w.ept_kf[e] = kf_id;
+            w.ept_obs[2 * e] = p->obs_list[i][0];
+            w.ept_obs[2 * e + 1] = p->obs_list[i][1];
+            const float invSigma2 = 1.0 / p->sigma_list[i];  // const float& (:6009)
+            w.ept_info[e] = (double)invSigma2;
+            w.ept_obs_idx[e] = (int)i;
+        }
+    }
+    // line vertices + edges (:6029-6117)
+    for (size_t li = 0, e = 0; li < nln; ++li) {
+        MapLine *l = w.local_ls[li];
+        w.ln_id[li] = l->idx;  // + maxPointId + 1 below
+        const size_t no = l->kf_obs_list.size();
+        for (size_t i = 0; i < no; ++i, ++e) {
+            const int kf_id = l->kf_obs_list[i];
+            if (kf_id < 0 || kf_id >= nkf_map || !valid[kf_id]) {
+                setError("[Wrong index in the map_keyframes and MapLine obs] line %d obs kf %d", l->idx, kf_id);
+                w.clear();
+                return PLBA_E_INVALID;
+            }
+            observer[kf_id] = 1;
+            w.eln_lm[e] = (int32_t)li;
+            w.eln_kf[e] = kf_id;
+            for (int k = 0; k < 4; ++k) w.eln_obs[4 * e + k] = l->NDw_obs_list[i][k];
+            const float invSigma2 = 1.0 / l->sigma_list[i];  // (:6073)
+            w.eln_info[e] = (double)invSigma2;
+            w.eln_obs_idx[e] = (int)i;
+        }
+        const Vec4 o = MapLine::changePlukerToOrth(l->NDw);
+        for (int k = 0; k < 4; ++k) w.ln_orth[li * 4 + k] = o[k];
+    }
+
+    std::map<int, KeyFrame *> idx_fix_kfs, idx_nofix_kfs, idx_all_kfs;  // one entry per KF (~100)
     for (auto *k : map_keyframes)  // :5870-5875
         if (k && k->local) {
             idx_nofix_kfs.insert({k->kf_idx, k});
             idx_all_kfs.insert({k->kf_idx, k});
         }
-    for (auto *p : map_points)
-        if (p && p->local) w.local_pt.push_back(p);  // :5877-5881
-    for (auto *l : map_lines)
-        if (l && l->local) w.local_ls.push_back(l);  // :5882-5886
     // observers outside the local set become fixed — and local, as a side effect (:5888-5919)
-    auto add_observers = [&](const std::vector<int> &obs) {
-        for (int o : obs) {
+    for (int o = 0; o < nkf_map; ++o)
+        if (observer[o]) {
             KeyFrame *k = map_keyframes[o];
             if (!k->local) {
                 idx_fix_kfs.insert({o, k});
@@ -269,11 +340,12 @@ int MapHandler::gatherWindow(Window &w) {
                 k->local = true;
             }
         }
-    };
-    for (auto *p : w.local_pt) add_observers(p->kf_obs_list);
-    for (auto *l : w.local_ls) add_observers(l->kf_obs_list);
 
     // pose vertices: free KFs (id 0 fixed), then the fixed observers (:5931-5967)
+    const size_t nkf = idx_nofix_kfs.size() + idx_fix_kfs.size();
+    w.kf_Tcw.reserve(nkf * 12);
+    w.kf_fixed.reserve(nkf);
+    w.kf_id.reserve(nkf);
     std::map<int, int> kf_pos;  // kf_idx -> position in the kf arrays
     auto add_pose = [&](KeyFrame *k, bool fixed) {
         const Mat4 Tcw = inverse4(k->T_kf_w);
@@ -292,55 +364,68 @@ int MapHandler::gatherWindow(Window &w) {
         w.fix_kfs.push_back(kv.second);
         add_pose(kv.second, true);
     }
-
-    // point vertices + edges (:5976-6027)
+    // observer id -> (kf_pos.at(id), idx_all_kfs.at(id)); every observer is in both maps
+    std::vector<int> pos_of(nkf_map, -1);
+    std::vector<KeyFrame *> kf_of(nkf_map, nullptr);
+    for (int o = 0; o < nkf_map; ++o)
+        if (observer[o]) {
+            pos_of[o] = kf_pos.at(o);
+            kf_of[o] = idx_all_kfs.at(o);
+        }
+    w.ept_kfp.resize(n_ept);
+    for (size_t i = 0; i < n_ept; ++i) {
+        const int o = w.ept_kf[i];
+        w.ept_kf[i] = pos_of[o];
+        w.ept_kfp[i] = kf_of[o];
+    }
+    w.eln_kfp.resize(n_eln);
+    for (size_t i = 0; i < n_eln; ++i) {
+        const int o = w.eln_kf[i];
+        w.eln_kf[i] = pos_of[o];
+        w.eln_kfp[i] = kf_of[o];
+    }
+    // vertex ids: point idx + max_kf_id + 1; line idx + maxPointId + 1 with maxPointId = the last
+    // point's id + 1 (`if (maxPointId < id + 1);` — the condition is a no-op, :6025-6026)
     w.maxPointId = w.max_kf_id;
-    for (size_t li = 0; li < w.local_pt.size(); ++li) {
-        MapPoint *p = w.local_pt[li];
-        const int id = p->idx + w.max_kf_id + 1;
-        w.pt_id.push_back(id);
-        for (int k = 0; k < 3; ++k) w.pt_xyz.push_back(p->point3D[k]);
-        for (size_t i = 0; i < p->kf_obs_list.size(); ++i) {
-            const int kf_id = p->kf_obs_list[i];
-            w.ept_lm.push_back((int32_t)li);
-            w.ept_kf.push_back(kf_pos.at(kf_id));
-            w.ept_obs.push_back(p->obs_list[i][0]);
-            w.ept_obs.push_back(p->obs_list[i][1]);
-            const float invSigma2 = 1.0 / p->sigma_list[i];  // const float& (:6009)
-            w.ept_info.push_back((double)invSigma2);
-            w.ept_kfp.push_back(idx_all_kfs.at(kf_id));
-            w.ept_obs_idx.push_back((int)i);
-        }
-        w.maxPointId = id + 1;  // `if (maxPointId < id + 1);` — the condition is a no-op (:6025-6026)
-    }
-    // line vertices + edges (:6029-6117)
-    for (size_t li = 0; li < w.local_ls.size(); ++li) {
-        MapLine *l = w.local_ls[li];
-        const int id = l->idx + w.maxPointId + 1;
-        w.ln_id.push_back(id);
-        const Vec4 o = MapLine::changePlukerToOrth(l->NDw);
-        for (int k = 0; k < 4; ++k) w.ln_orth.push_back(o[k]);
-        for (size_t i = 0; i < l->kf_obs_list.size(); ++i) {
-            const int kf_id = l->kf_obs_list[i];
-            w.eln_lm.push_back((int32_t)li);
-            w.eln_kf.push_back(kf_pos.at(kf_id));
-            for (int k = 0; k < 4; ++k) w.eln_obs.push_back(l->NDw_obs_list[i][k]);
-            const float invSigma2 = 1.0 / l->sigma_list[i];  // (:6073)
-            w.eln_info.push_back((double)invSigma2);
-            w.eln_kfp.push_back(idx_all_kfs.at(kf_id));
-            w.eln_obs_idx.push_back((int)i);
-        }
-    }
+    for (auto &id : w.pt_id) id += w.max_kf_id + 1;
+    if (npt) w.maxPointId = w.pt_id[npt - 1] + 1;
+    for (auto &id : w.ln_id) id += w.maxPointId + 1;
     // g2o::SparseOptimizer::addVertex refuses a duplicate id; refuse the window instead
-    std::vector<int32_t> ids(w.kf_id);
-    ids.insert(ids.end(), w.pt_id.begin(), w.pt_id.end());
-    ids.insert(ids.end(), w.ln_id.begin(), w.ln_id.end());
-    std::sort(ids.begin(), ids.end());
-    if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) {
+    if (has_duplicate_id(w)) {
         setError("duplicate g2o vertex id in the window");
         return PLBA_E_INVALID;
     }
     return PLBA_OK;
+}
+
+// any id shared by two vertices of the window: a bitmap over [min, max] when the range is
+// comparable to the vertex count, a sort otherwise
+static bool has_duplicate_id(const Window &w) {
+    const std::vector<int32_t> *lists[3] = {&w.kf_id, &w.pt_id, &w.ln_id};
+    size_t n = 0;
+    long long lo = 0, hi = -1;
+    for (auto *v : lists)
+        for (int32_t id : *v) {
+            if (n++ == 0) lo = hi = id;
+            lo = std::min<long long>(lo, id);
+            hi = std::max<long long>(hi, id);
+        }
+    if (n < 2) return false;
+    if (hi - lo + 1 <= (long long)(16 * n + 4096)) {
+        std::vector<uint8_t> seen((size_t)(hi - lo + 1), 0);
+        for (auto *v : lists)
+            for (int32_t id : *v) {
+                uint8_t &s = seen[(size_t)(id - lo)];
+                if (s) return true;
+                s = 1;
+            }
+        return false;
+    }
+    std::vector<int32_t> ids;
+    ids.reserve(n);
+    for (auto *v : lists) ids.insert(ids.end(), v->begin(), v->end());
+    std::sort(ids.begin(), ids.end());
+    return std::adjacent_find(ids.begin(), ids.end()) != ids.end();
 }
 
 int MapHandler::ensureCtx() {
@@ -474,7 +559,7 @@ int MapHandler::localBundleAdjustmentForPlukerWithG2O(LbaStats *stats) {
     using clk = std::chrono::steady_clock;
     LbaStats st;
     const auto t0 = clk::now();
-    Window w;
+    Window &w = win_;
     int rc = gatherWindow(w);
     if (rc) return rc;
     const plba_graph g = w.graph(fx_, fy_, cx_, cy_);
@@ -482,9 +567,12 @@ int MapHandler::localBundleAdjustmentForPlukerWithG2O(LbaStats *stats) {
     st.n_fixed_kf = (int)w.fix_kfs.size();
     st.n_pt = g.n_pt; st.n_ln = g.n_ln; st.n_ept = g.n_ept; st.n_eln = g.n_eln;
 
-    std::vector<double> Tcw(w.kf_Tcw.size()), xyz(w.pt_xyz.size()), orth(w.ln_orth.size());
-    std::vector<double> ept_chi2(g.n_ept), eln_chi2(g.n_eln);
-    std::vector<uint8_t> ept_depth(g.n_ept), ept_level(g.n_ept), eln_level(g.n_eln);
+    std::vector<double> &Tcw = out_Tcw_, &xyz = out_xyz_, &orth = out_orth_, &ept_chi2 = out_ept_chi2_,
+                        &eln_chi2 = out_eln_chi2_;
+    std::vector<uint8_t> &ept_depth = out_ept_depth_, &ept_level = out_ept_level_, &eln_level = out_eln_level_;
+    Tcw.resize(w.kf_Tcw.size()); xyz.resize(w.pt_xyz.size()); orth.resize(w.ln_orth.size());
+    ept_chi2.resize(g.n_ept); eln_chi2.resize(g.n_eln);
+    ept_depth.resize(g.n_ept); ept_level.resize(g.n_ept); eln_level.resize(g.n_eln);
     plba_result r{};
     r.kf_Tcw = Tcw.data(); r.pt_xyz = xyz.data(); r.ln_orth = orth.data();
     r.ept_chi2 = ept_chi2.data(); r.ept_depth_ok = ept_depth.data(); r.ept_level = ept_level.data();

@@ -105,6 +105,9 @@ struct Window {
     std::vector<KeyFrame *> ept_kfp, eln_kfp;
     std::vector<int> ept_obs_idx, eln_obs_idx;
     plba_graph graph(double fx, double fy, double cx, double cy) const;
+    // empty, keeping every array's capacity (a MapHandler reuses one Window across calls: the
+    // arrays of a C3 window are ~6 MB, and fresh pages cost more than filling them)
+    void clear();
 };
 
 struct LbaStats {
@@ -230,6 +233,10 @@ class MapHandler {
     void *pgo_user_ = nullptr;
     int loopClosurePGO(bool ess, PgoStats *stats);
     std::string err_;
+    // per-call scratch reused across LBA calls (capacity kept; see Window::clear)
+    Window win_;
+    std::vector<double> out_Tcw_, out_xyz_, out_orth_, out_ept_chi2_, out_eln_chi2_;
+    std::vector<uint8_t> out_ept_depth_, out_ept_level_, out_eln_level_;
 };
 
 // helpers (host restatements)

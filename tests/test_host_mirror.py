@@ -175,6 +175,23 @@ def test_inconsistent_map_is_refused_and_untouched(window):
     assert [k.local for k in after.keyframes] == [k.local for k in bad.keyframes]
 
 
+def test_inconsistent_line_observation_is_refused_and_untouched(window):
+    """The single-pass gather checks line observations after every point's (the reference's
+    order, src/mapHandler.cpp:5891-5911) and leaves the local flags untouched."""
+    m = make_map(window, seed=7)
+    bad = m.copy()
+    ln = [l for l in bad.lines if l is not None and l.local]
+    if not ln:
+        pytest.skip("window without lines")
+    ln[-1].kf_obs_list[-1] = -3
+    hmap, seen = host_with(bad, stub_solve)
+    with pytest.raises(Exception, match="MapLine obs"):
+        hmap.local_ba()
+    assert "graph" not in seen
+    after = hmap.read(bad)
+    assert [k.local for k in after.keyframes] == [k.local for k in bad.keyframes]
+
+
 def test_solver_failure_leaves_map_untouched(window):
     m = make_map(window, seed=6)
     hmap = HostMap(m)
