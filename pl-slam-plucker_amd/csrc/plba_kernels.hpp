@@ -419,8 +419,18 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
     const int nxt = cc->stage + 1;
     const int robust = sw ? cc->stage_robust[nxt] : cc->robust;
     double *chi2e = chi2cur(d);  // this iteration's χ² go where the last consumed trial's are
+#ifndef PLBA_LIN_DIRECT
+    // A/c/B rows are staged in LDS and written out as contiguous 1-KB pieces per store instruction:
+    // written per lane (96/16/64-B rows at a lane stride) every store instruction of a wave touched
+    // ~48 cache lines, and the stores of the long line-edge waves were the kernel's tail
+    __shared__ __attribute__((aligned(16))) double stA[kBlock * 12], stc[kBlock * 2], stB[kBlock * 8];
+#endif
     if (e < d.E) {
+#ifndef PLBA_LIN_DIRECT
+        double *A = stA + threadIdx.x * 12, *c = stc + threadIdx.x * 2, *B = stB + threadIdx.x * 8;
+#else
         double *A = d.A + (size_t)e * 12, *c = d.cvec + (size_t)e * 2, *B = d.B + (size_t)e * 8;
+#endif
         if (sw) {
             const double stale = chi2e[e];
             // every χ² buffer starts the stage with the stale values: an edge the new stage leaves
@@ -536,6 +546,20 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
             for (int k = 0; k < 8; ++k) B[k] = 0.0;
         }
     }
+#ifndef PLBA_LIN_DIRECT
+    __syncthreads();
+    {
+        const int e0 = blockIdx.x * kBlock, n = min(kBlock, d.E - e0);
+        auto copy_out = [&](const double *src, double *dst, int cnt) {  // cnt doubles, even
+            const double2 *s2 = reinterpret_cast<const double2 *>(src);
+            double2 *d2 = reinterpret_cast<double2 *>(dst);
+            for (int t = threadIdx.x; t < cnt / 2; t += kBlock) d2[t] = s2[t];
+        };
+        copy_out(stA, d.A + (size_t)e0 * 12, n * 12);
+        copy_out(stc, d.cvec + (size_t)e0 * 2, n * 2);
+        copy_out(stB, d.B + (size_t)e0 * 8, n * 8);
+    }
+#endif
     double s = block_sum<kBlock>(rc, sh);
     if (threadIdx.x == 0) d.part_chi2[blockIdx.x] = s;
 }
@@ -843,13 +867,17 @@ __device__ __forceinline__ void iter_init_ctrl(const Dev &d, double chi, double 
             c->need_iter = 0;
             return;
         }
-        c->currentChi = chi;
-        c->chi2_start = chi;
+        // currentChi: at iteration 0 the χ² of the linearisation; later iterations start at the
+        // state of the trial just accepted, whose χ² (the same edges at the same state, summed in
+        // another order) is already currentChi — kept, so the folded init can skip its global
+        // reduction after the first iteration (k_iter_reduce) and every mode agrees
         if (c->iter == 0) {  // computeLambdaInit: τ·max|H_jj|, ν = 2
+            c->currentChi = chi;
             c->maxdiag = mx;
             c->lambda = d.tau * mx;
             c->ni = 2.0;
         }
+        c->chi2_start = c->currentChi;
         c->lambda_start = c->lambda;
         c->qmax = 0;
         c->accept = 0;
@@ -865,6 +893,13 @@ __global__ __launch_bounds__(kInitNT) void k_iter_init(Dev d) {
 }
 
 constexpr int kRedGrp = 256;  // k_iter_reduce workgroups per first-level group of the folded init
+// an iteration after the first of its stage (g2o Levenberg, not the hand-rolled LM, unsharded,
+// folded init): k_decide has already done the iteration init (decide_body), so k_iter_reduce only
+// forms Hpp / b_p / Hll / b_l. Uniform: read before any workgroup can change the control block.
+__device__ __forceinline__ bool iter_init_fast(const Dev &d) {
+    const Ctrl *c = d.ctrl;
+    return d.fold_init && !d.sharded && !c->hlm && !c->switch_pending && c->iter > 0;
+}
 __global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
     ITER_GUARD
     __shared__ double sh_init[kLmBlock / 64];
@@ -873,7 +908,7 @@ __global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
     // folded init: this workgroup's slice of k_linearize's χ² partials, loaded before the main
     // work so the round trip overlaps it
     double sc = 0.0;
-    if (d.fold_init) {
+    if (d.fold_init && !iter_init_fast(d)) {
         const int lo = (int)((long long)b * d.n_lin_blocks / G), hi = (int)((long long)(b + 1) * d.n_lin_blocks / G);
         for (int i = lo + lane; i < hi; i += kLmBlock) sc += d.part_chi2[i];
     }
@@ -882,6 +917,9 @@ __global__ __launch_bounds__(kLmBlock) void k_iter_reduce(Dev d) {
     if (b < np) wmax = pose_partial(d, b / kPoseParts, b % kPoseParts);  // workgroup-uniform branch
     else landmark_reduce(d, b - np, wmax, wany);
     if (!d.fold_init) return;
+    // after the first iteration of a stage the init needs none of the global terms (λ is set, the
+    // χ² is the accepted trial's, no activity change): k_decide already started the iteration
+    if (iter_init_fast(d)) return;
     // folded iteration init (k_iter_init's work; the pose combine already ran per pose), reduced
     // in two levels so no single workgroup reads every partial: each workgroup adds a slice of
     // k_linearize's χ² partials to its own (max, any), the last of each group of kRedGrp
@@ -2102,7 +2140,7 @@ __device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, bool mu
             double sj = H[pk(j, j)] + (mul ? lam * H[pk(j, j)] : lam);
 #pragma unroll
             for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
-            const double djj = sqrt(sj);
+            const double djj = 1.0 / sqrt(sj);  // reciprocal diagonal: every use divides by it
             L[pk(j, j)] = djj;
 #pragma unroll
             for (int i = j + 1; i < 4; ++i) {
@@ -2110,7 +2148,7 @@ __device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, bool mu
                     double t = H[pk(i, j)];
 #pragma unroll
                     for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
-                    L[pk(i, j)] = t / djj;
+                    L[pk(i, j)] = t * djj;
                 }
             }
         }
@@ -2121,15 +2159,14 @@ __device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, bool mu
             double t = d.bl[(size_t)l * 4 + i];
 #pragma unroll
             for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * g[p];
-            g[i] = t / L[pk(i, i)];
+            g[i] = t * L[pk(i, i)];
         }
     }
 }
-// per edge: Z_e = B_e L⁻ᵀ (rows solved with L), q_e = Z_e g
-__global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d0) {
-    TRIAL_SLOT(blockIdx.y)
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    if (e >= d.E) return;
+// per edge: Z_e = B_e L⁻ᵀ (rows solved with L), q_e = Z_e g. The Z / q rows are staged in LDS and
+// written out as contiguous pieces (per-lane 64-B / 16-B rows made every store instruction touch
+// ~32 cache lines; see k_linearize)
+__device__ __forceinline__ void edge_schur_body(const Dev &d, int e, double *Z, double *qe) {
     const int l = d.e_lm[e];
     if (e >= d.Ep && d.ctrl->hlm == 2) {  // GBA line: 6x6 (Hl6 + λ·diag) = L Lᵀ, Z_e = L⁻¹ b_e, q_e = Z_e·L⁻¹ b_l
         const double lam = d.lam;
@@ -2167,12 +2204,11 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d0) {
             g6[i] = tg / L6[pk(i, i)];
             q0 += z[i] * g6[i];
         }
-        double *Z = d.Z + (size_t)e * 8;
 #pragma unroll
         for (int k = 0; k < 6; ++k) Z[k] = z[k];
         Z[6] = Z[7] = 0.0;
-        d.q[(size_t)e * 2 + 0] = q0;
-        d.q[(size_t)e * 2 + 1] = 0.0;
+        qe[0] = q0;
+        qe[1] = 0.0;
         return;
     }
     const int DIM = e < d.Ep ? 3 : 4;
@@ -2189,10 +2225,9 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d0) {
                 double t = B[r * 4 + i];
 #pragma unroll
                 for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * z[r][p];
-                z[r][i] = t / L[pk(i, i)];
+                z[r][i] = t * L[pk(i, i)];
             }
         }
-    double *Z = d.Z + (size_t)e * 8;
     double q0 = 0, q1 = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2201,8 +2236,30 @@ __global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d0) {
         q0 += z[0][i] * g[i];
         q1 += z[1][i] * g[i];
     }
-    d.q[(size_t)e * 2 + 0] = q0;
-    d.q[(size_t)e * 2 + 1] = q1;
+    qe[0] = q0;
+    qe[1] = q1;
+}
+__global__ __launch_bounds__(kBlock) void k_edge_schur(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+#ifdef PLBA_SCHUR_DIRECT
+    if (e < d.E) edge_schur_body(d, e, d.Z + (size_t)e * 8, d.q + (size_t)e * 2);
+#else
+    __shared__ __attribute__((aligned(16))) double stZ[kBlock * 8], stq[kBlock * 2];
+    if (e < d.E) edge_schur_body(d, e, stZ + threadIdx.x * 8, stq + threadIdx.x * 2);
+    __syncthreads();
+    const int e0 = blockIdx.x * kBlock, n = min(kBlock, d.E - e0);
+    {
+        const double2 *s2 = reinterpret_cast<const double2 *>(stZ);
+        double2 *d2 = reinterpret_cast<double2 *>(d.Z + (size_t)e0 * 8);
+        for (int t = threadIdx.x; t < n * 4; t += kBlock) d2[t] = s2[t];
+    }
+    {
+        const double2 *s2 = reinterpret_cast<const double2 *>(stq);
+        double2 *d2 = reinterpret_cast<double2 *>(d.q + (size_t)e0 * 2);
+        for (int t = threadIdx.x; t < n; t += kBlock) d2[t] = s2[t];
+    }
+#endif
 }
 // per landmark: x_l = L⁻ᵀ L⁻¹ (b_l - Σ u_e), oplus into the trial state, scale partial
 // quad (4-lane) DPP exchanges: xor 1 = quad_perm [1,0,3,2], xor 2 = quad_perm [2,3,0,1]
@@ -2429,6 +2486,7 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
     }
     const int cur0 = c->cur, lo0 = c->last_ok, ch0 = c->chi_src;
     bool any_ok = false, hold = false, trials_go_on = false, done = false;
+    c->need_iter = 0;  // (iter_init_ctrl's reset when k_iter_reduce took the fast path)
 #pragma unroll
     for (int s = 0; s < kMaxSpec; ++s) {
         if (done || s >= W) continue;
@@ -2488,7 +2546,15 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
             if (c->stage + 1 < c->n_stages) c->switch_pending = 1;
             else c->all_done = 1;
         } else {
+            // the next iteration's init (iter_init_ctrl with iter > 0), done here so that
+            // k_iter_reduce can skip its global reduction (iter_init_fast)
             c->need_iter = 1;
+            c->chi2_start = c->currentChi;
+            c->lambda_start = c->lambda;
+            c->qmax = 0;
+            c->accept = 0;
+            c->rho = 0.0;
+            c->broke = 0;
         }
     }
     // the next step's trial slots (Dev::spec_policy)
@@ -2650,7 +2716,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
                         double sj = H[pk(j, j)] + (hlm ? lam * H[pk(j, j)] : lam);
 #pragma unroll
                         for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
-                        const double djj = sqrt(sj);
+                        const double djj = 1.0 / sqrt(sj);  // reciprocal diagonal (as lm_chol)
                         L[pk(j, j)] = djj;
 #pragma unroll
                         for (int i = j + 1; i < 4; ++i) {
@@ -2658,7 +2724,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
                                 double t = H[pk(i, j)];
 #pragma unroll
                                 for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
-                                L[pk(i, j)] = t / djj;
+                                L[pk(i, j)] = t * djj;
                             }
                         }
                     }
@@ -2670,7 +2736,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
                         double t = bl[i] - u[i];
 #pragma unroll
                         for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * y[p];
-                        y[i] = t / L[pk(i, i)];
+                        y[i] = t * L[pk(i, i)];
                     }
 #pragma unroll
                 for (int i = 3; i >= 0; --i)
@@ -2679,7 +2745,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
 #pragma unroll
                         for (int p = i + 1; p < 4; ++p)
                             if (p < DIM) t -= L[pk(p, i)] * x[p];
-                        x[i] = t / L[pk(i, i)];
+                        x[i] = t * L[pk(i, i)];
                     }
                 if (q == 0) {
 #pragma unroll

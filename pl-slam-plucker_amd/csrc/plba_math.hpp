@@ -139,8 +139,14 @@ PLBA_HD void point_pc(const double *T, const double *P, double *Pc) {
 PLBA_HD void point_error(const double *T, const double *P, const double *obs, const Cam &c, double *e, double &z) {
     double Pc[3];
     point_pc(T, P, Pc);
+#ifdef PLBA_EXACT_DIV
     double u = (Pc[0] / Pc[2]) * c.fx + c.cx;
     double v = (Pc[1] / Pc[2]) * c.fy + c.cy;
+#else
+    const double iz = 1.0 / Pc[2];  // one reciprocal (within ~1 ulp of the two divisions)
+    double u = (Pc[0] * iz) * c.fx + c.cx;
+    double v = (Pc[1] * iz) * c.fy + c.cy;
+#endif
     e[0] = obs[0] - u;
     e[1] = obs[1] - v;
     z = Pc[2];
@@ -151,7 +157,11 @@ PLBA_HD void point_jac(const double *T, const double *P, const Cam &c, double *J
     point_pc(T, P, Pc);
     double x = Pc[0], y = Pc[1], z = Pc[2];
     double invz = 1.0 / z, invz2 = invz * invz;
+#ifdef PLBA_EXACT_DIV
     const double J[6] = {c.fx / z, 0, -c.fx * x * invz2, 0, c.fy / z, -c.fy * y * invz2};
+#else
+    const double J[6] = {c.fx * invz, 0, -c.fx * x * invz2, 0, c.fy * invz, -c.fy * y * invz2};
+#endif
     const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
 #pragma unroll
     for (int r = 0; r < 2; ++r)
@@ -190,8 +200,14 @@ PLBA_HD void line_error(const double *T, const double *L, const double *obs, con
     double l[3];
     line_image(T, L, c, l);
     double f = sqrt(l[0] * l[0] + l[1] * l[1]);
+#ifdef PLBA_EXACT_DIV
     e[0] = (l[0] * obs[0] + l[1] * obs[1] + l[2]) / f;
     e[1] = (l[0] * obs[2] + l[1] * obs[3] + l[2]) / f;
+#else
+    const double invf = 1.0 / f;
+    e[0] = (l[0] * obs[0] + l[1] * obs[1] + l[2]) * invf;
+    e[1] = (l[0] * obs[2] + l[1] * obs[3] + l[2]) * invf;
+#endif
 }
 // Jl: 2x4 (row-major), Jp: 2x6 ; also returns the error
 PLBA_HD void line_jac(const double *T, const double *orth, const double *L, const double *obs, const Cam &c,
@@ -202,12 +218,24 @@ PLBA_HD void line_jac(const double *T, const double *orth, const double *L, cons
     line_image(T, L, c, l);
     double lx = l[0], ly = l[1], lz = l[2];
     double f = sqrt(lx * lx + ly * ly);
+#ifdef PLBA_EXACT_DIV
     double e0 = (lx * obs[0] + ly * obs[1] + lz) / f;
     double e1 = (lx * obs[2] + ly * obs[3] + lz) / f;
     e[0] = e0;
     e[1] = e1;
     const double j[2][3] = {{-lx * e0 / (f * f) + obs[0] / f, -ly * e0 / (f * f) + obs[1] / f, 1.0 / f},
                             {-lx * e1 / (f * f) + obs[2] / f, -ly * e1 / (f * f) + obs[3] / f, 1.0 / f}};
+#else
+    // one reciprocal per distinct denominator (an IEEE division is a ~10-instruction dependent
+    // chain, and this edge type is the linearisation's longest wave): within ~1 ulp of a / b
+    const double invf = 1.0 / f, invf2 = invf * invf;
+    double e0 = (lx * obs[0] + ly * obs[1] + lz) * invf;
+    double e1 = (lx * obs[2] + ly * obs[3] + lz) * invf;
+    e[0] = e0;
+    e[1] = e1;
+    const double j[2][3] = {{-lx * e0 * invf2 + obs[0] * invf, -ly * e0 * invf2 + obs[1] * invf, invf},
+                            {-lx * e1 * invf2 + obs[2] * invf, -ly * e1 * invf2 + obs[3] * invf, invf}};
+#endif
     const double K[9] = {c.fy, 0, 0, 0, c.fx, 0, -c.fy * c.cx, -c.fx * c.cy, c.fx * c.fy};
     double jK[2][3];
 #pragma unroll
@@ -243,14 +271,25 @@ PLBA_HD void line_jac(const double *T, const double *orth, const double *L, cons
     double cr[3] = {L[1] * L[5] - L[2] * L[4], L[2] * L[3] - L[0] * L[5], L[0] * L[4] - L[1] * L[3]};
     double cn = sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
     double fw = sqrt(nn * nn + dn * dn);
-    double w1 = nn / fw, w2 = dn / fw;
     double u1[3], u2[3], u3[3];
+#ifdef PLBA_EXACT_DIV
+    double w1 = nn / fw, w2 = dn / fw;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         u1[i] = L[i] / nn;
         u2[i] = L[3 + i] / dn;
         u3[i] = cr[i] / cn;
     }
+#else
+    const double ifw = 1.0 / fw, inn = 1.0 / nn, idn = 1.0 / dn, icn = 1.0 / cn;
+    double w1 = nn * ifw, w2 = dn * ifw;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        u1[i] = L[i] * inn;
+        u2[i] = L[3 + i] * idn;
+        u3[i] = cr[i] * icn;
+    }
+#endif
     double StR[9];
     mat3mul(St, R, StR);
 #pragma unroll
