@@ -573,6 +573,9 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
 //   workgroups [kPoseParts·nf, ...): 64 landmarks each, Hll = Σ B_eᵀB_e, b_l = Σ B_eᵀc_e
 //     (and, on a stage switch, the landmark activation).
 constexpr int kPoseParts = 4;
+#ifndef PLBA_POSE_KU
+#define PLBA_POSE_KU 4  // pose-part edges with loads in flight per pass
+#endif
 constexpr int kPP = 28;        // per pose part: 21 (upper Σ AᵀA) + 6 (Σ Aᵀc) + active-edge count
 constexpr int kInitNT = 1024;  // k_iter_init / k_iter_pack: one wide workgroup (the pose combine)
 
@@ -586,7 +589,7 @@ __device__ __forceinline__ double pose_partial(const Dev &d, int h, int part) {
     for (int k = 0; k < kPP; ++k) acc[k] = 0.0;
     // kU edges per pass with all their loads issued before the arithmetic (the per-thread
     // chains are edge-index -> A/c misses; one edge at a time leaves them serialised)
-    constexpr int S = kPoseParts * 64, kU = 4;
+    constexpr int S = kPoseParts * 64, kU = PLBA_POSE_KU;
     const int pend = d.pe_off[h + 1];
     for (int p0 = d.pe_off[h] + part * 64 + threadIdx.x; p0 < pend; p0 += kU * S) {
         int ei[kU];
@@ -616,6 +619,7 @@ __device__ __forceinline__ double pose_partial(const Dev &d, int h, int part) {
             for (int r = 0; r < 6; ++r) acc[21 + r] += a0[r] * cv[j][0] + a1[r] * cv[j][1];
         }
     }
+#ifdef PLBA_POSE_WAVESUM
 #pragma unroll
     for (int k = 0; k < kPP; ++k) acc[k] = wave_sum(acc[k]);
     if (threadIdx.x == 0) {
@@ -623,6 +627,30 @@ __device__ __forceinline__ double pose_partial(const Dev &d, int h, int part) {
 #pragma unroll
         for (int k = 0; k < kPP; ++k) st_sc1(o + k, acc[k]);  // read by the pose's combine below
     }
+#else
+    {
+        // the 28 sums as a reduce-scatter: each butterfly step halves the values a lane carries
+        // (~220 instead of ~500 instructions); value k ends in lane 2k. The same pairwise
+        // additions as wave_sum (a + b in the same butterfly order), so bitwise the same sums.
+        const int lane = threadIdx.x;
+        double v[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) v[k] = k < kPP ? acc[k] : 0.0;
+#pragma unroll
+        for (int n = 16; n >= 1; n >>= 1) {
+            const int m = 2 * n;  // lane bit of this step: 32, 16, 8, 4, 2
+            const bool hi = (lane & m) != 0;
+#pragma unroll
+            for (int i = 0; i < n; ++i) {
+                const double keep = hi ? v[n + i] : v[i], send = hi ? v[i] : v[n + i];
+                v[i] = keep + __shfl_xor(send, m, 64);
+            }
+        }
+        v[0] += __shfl_xor(v[0], 1, 64);
+        if ((lane & 1) == 0 && lane / 2 < kPP)
+            st_sc1(d.pose_part + ((size_t)h * kPoseParts + part) * kPP + lane / 2, v[0]);  // read by the combine below
+    }
+#endif
     // folded iteration init: the last of the pose's kPoseParts workgroups adds the parts (in part
     // order, as pose_combine does) into Hpp / b_p / active count and publishes max|Hpp_jj|
     // (sharded windows too: the combine then writes this rank's partial Hpp / b_p into the
