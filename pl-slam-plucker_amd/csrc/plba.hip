@@ -637,6 +637,13 @@ std::vector<int32_t> rcm_from_adj(std::vector<std::vector<int32_t>> &adj) {
     return best;
 }
 
+int allreduce(plba_ctx *ctx, const double *send, double *recv, size_t n);
+// Sharded windows: the RCS exchange. PLBA_SHARD_XCHG=allreduce restores the all-reduce of the
+// whole partial system (A/B runs); the default all-gathers each rank's nonzero runs.
+inline bool xchg_gather() {
+    const char *e = getenv("PLBA_SHARD_XCHG");
+    return !(e && std::string(e) == "allreduce");
+}
 int do_upload(plba_ctx *ctx, const plba_graph *g) {
     if (!g || g->n_kf < 0 || g->n_pt < 0 || g->n_ln < 0 || g->n_ept < 0 || g->n_eln < 0) {
         ctx->set_error("invalid graph sizes");
@@ -1049,6 +1056,46 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
                 X[(size_t)(n_pt + l) * 4 + k] = g->ln_orth[4 * (size_t)(lm_gpos[n_pt + l] - n_pt_g) + k];
     }
 
+    // sharded, all-gather exchange: this rank's block-row range [lo, hi] (rows of the blocks that
+    // hold one of its Schur triples — every local edge of a free pose has its diagonal triple), as
+    // two runs of red_rcs; every rank's runs are exchanged here, so all ranks size the same record
+    std::vector<int64_t> xg_rng;
+    int64_t xg_P = 0;
+    if (sharded && nblk > 0 && xchg_gather()) {
+        int lo = nf, hi = -1;
+        for (int b = 0; b < nblk; ++b)
+            if (blk_off[b + 1] > blk_off[b]) {
+                lo = std::min(lo, blk_i2[b]);
+                hi = std::max(hi, blk_i2[b]);
+            }
+        std::vector<double> mine(4 * (size_t)R, 0.0);
+        if (hi >= lo) {
+            mine[4 * rank + 0] = (double)(blk_base[lo] * 36);
+            mine[4 * rank + 1] = (double)((blk_base[hi + 1] - blk_base[lo]) * 36);
+            mine[4 * rank + 2] = (double)((int64_t)nblk * 36 + 6 * (int64_t)lo);
+            mine[4 * rank + 3] = (double)(6 * (int64_t)(hi - lo + 1));
+        }
+        double *tmp = nullptr;
+        PLBA_CHECK(hipMallocAsync((void **)&tmp, mine.size() * sizeof(double), ctx->stream));
+        PLBA_CHECK(hipMemcpyAsync(tmp, mine.data(), mine.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+        int xrc = allreduce(ctx, tmp, tmp, mine.size());
+        if (!xrc) {
+            xrc = hipMemcpyAsync(mine.data(), tmp, mine.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) ==
+                          hipSuccess && hipStreamSynchronize(ctx->stream) == hipSuccess
+                      ? PLBA_OK : PLBA_E_DEVICE;
+        }
+        (void)hipFreeAsync(tmp, ctx->stream);
+        if (xrc) {
+            if (xrc == PLBA_E_DEVICE) ctx->set_error("shard range exchange: device copy failed");
+            return xrc;
+        }
+        xg_rng.resize(4 * (size_t)R);
+        for (int r = 0; r < R; ++r) {
+            for (int k = 0; k < 4; ++k) xg_rng[4 * r + k] = (int64_t)mine[4 * r + k];
+            xg_P = std::max(xg_P, xg_rng[4 * r + 1] + xg_rng[4 * r + 3]);
+        }
+        xg_P = std::max<int64_t>(xg_P, 2);
+    }
     std::vector<int32_t> h_kf(bcr ? nf : 0, 0);
     for (int k = 0; k < n_kf && bcr; ++k)
         if (kf_hidx[k] >= 0) h_kf[kf_hidx[k]] = k;
@@ -1095,8 +1142,13 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.B, (size_t)E * 8);
     for (int b = 0; b < nbx; ++b) ZALLOC(d.chi2b[b], E);
     // Hpp | b_p | #active edges | χ² | active | landmark max per rank: one array, all-reduced when sharded
-    ALLOC(d.red_iter, (size_t)nf * 43 + 2 + R);
-    if (sharded) ALLOC(d.red_iter_loc, (size_t)nf * 43 + 2 + R);
+    // unsharded: Hpp | b_p | active | χ² | any | max; sharded: diag(Hpp) | b_p | active | χ² | any |
+    // per-rank maxima, all-reduced (the full partial Hpp stays local: Hpp_w)
+    ALLOC(d.red_iter, (size_t)nf * (sharded ? 13 : 43) + 2 + R);
+    if (sharded) {
+        ALLOC(d.red_iter_loc, (size_t)nf * 13 + 2 + R);
+        ALLOC(d.Hpp_w, (size_t)nf * 36);
+    }
     ALLOC(d.Hll, (size_t)n_lm * 10);
     ALLOC(d.bl, (size_t)n_lm * 4);
     // λ-dependent arrays: one copy per trial slot, back to back (slot_view, sl_* in plba_kernels.hpp)
@@ -1186,6 +1238,16 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ALLOC(d.red_rcs_loc, (size_t)nblk * 36 + (size_t)nf * 6);
         ALLOC(d.red_dec_loc, 3);  // + the hand-off error agreement slot (agree_dev_error)
     }
+    d.xg_P = 0;
+    d.xg_host = ctx->comm.kind == plba_ctx::Comm::HOST ? 1 : 0;
+    if (sharded && xg_rng.size()) {
+        d.xg_P = xg_P;
+        UPLOAD(d.xg_rng, xg_rng);
+        // zeroed once: blockpart rewrites the same in-run positions every step, the padding (and,
+        // host transport, the other ranks' slots) stays zero
+        ZALLOC(d.xg_send, (size_t)(d.xg_host ? R : 1) * xg_P);
+        ALLOC(d.xg_recv, (size_t)R * xg_P);
+    }
     // output maps (local landmark / edge -> whole-window position): the download scatter
     // (k_out_scatter) or, sharded, the final gather of the full window X | χ² | depth | level
     UPLOAD_D(d.lm_gpos, lm_gpos, wb.lm_gpos, n_lm);
@@ -1210,13 +1272,24 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.xp = d.xpb[0];
     d.xl = d.xlb[0];
     d.chi2_last = d.chi2b[0];
-    d.Hpp = d.red_iter;
-    d.bp = d.red_iter + (size_t)nf * 36;
-    d.pact = d.red_iter + (size_t)nf * 42;
-    if (!sharded) d.red_iter_loc = d.red_iter;
-    d.Hpp_w = d.red_iter_loc;
-    d.bp_w = d.red_iter_loc + (size_t)nf * 36;
-    d.pact_w = d.red_iter_loc + (size_t)nf * 42;
+    if (sharded) {
+        d.Hpp = nullptr;
+        d.Hdg = d.red_iter;
+        d.bp = d.red_iter + (size_t)nf * 6;
+        d.pact = d.red_iter + (size_t)nf * 12;
+        d.Hdg_w = d.red_iter_loc;
+        d.bp_w = d.red_iter_loc + (size_t)nf * 6;
+        d.pact_w = d.red_iter_loc + (size_t)nf * 12;
+    } else {
+        d.Hpp = d.red_iter;
+        d.bp = d.red_iter + (size_t)nf * 36;
+        d.pact = d.red_iter + (size_t)nf * 42;
+        d.red_iter_loc = d.red_iter;
+        d.Hpp_w = d.red_iter_loc;
+        d.bp_w = d.red_iter_loc + (size_t)nf * 36;
+        d.pact_w = d.red_iter_loc + (size_t)nf * 42;
+        d.Hdg = d.Hdg_w = nullptr;
+    }
     if (band_mode) PLBA_CHECK(hipFuncSetAttribute(band_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)band_lds_bytes(bw, nf)));
     if (bcr) {
@@ -1290,6 +1363,21 @@ int allreduce(plba_ctx *ctx, const double *send, double *recv, size_t n) {
     ctx->set_error("sharded window without a transport");
     return PLBA_E_COMM;
 }
+// All-gather of P doubles per rank: recv = [rank 0's P | rank 1's P | ...]. The host transport
+// only sums, so there each rank's send is its own slot of an R x P array, zero elsewhere.
+int allgather(plba_ctx *ctx, const double *send, double *recv, size_t P) {
+    auto &c = ctx->comm;
+    if (P == 0) return PLBA_OK;
+    if (c.kind == plba_ctx::Comm::RCCL) {
+        const ncclResult_t r = ncclAllGather(send, recv, P, ncclDouble, c.nccl, ctx->stream);
+        if (r != ncclSuccess) {
+            ctx->set_error("ncclAllGather(%zu doubles): %s", P, ncclGetErrorString(r));
+            return PLBA_E_COMM;
+        }
+        return PLBA_OK;
+    }
+    return allreduce(ctx, send, recv, (size_t)c.nranks * P);
+}
 #define COMM(send, recv, n)                                  \
     do {                                                     \
         int _rc = allreduce(ctx, (send), (recv), (size_t)(n)); \
@@ -1308,7 +1396,7 @@ int launch_step(plba_ctx *ctx) {
     }
     if (d.sharded) {
         LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kInitNT), 0, s, d));
-        COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 43 + 2 + d.nranks);
+        COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 13 + 2 + d.nranks);
     }
     const bool reduced = d.nf > 0 || d.n_lm > 0;
     if (!(d.fold_init && reduced))  // (folded into the last k_iter_reduce workgroup otherwise)
@@ -1321,7 +1409,12 @@ int launch_step(plba_ctx *ctx) {
         if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(chunk_direct ? k_rcs_chunk<false> : k_rcs_chunk<true>, dim3(8 * ((d.nch + 7) / 8), d.spec_max), dim3(64), 0, s, d));
         if (d.sharded) {
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
-            COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);
+            if (d.xg_P > 0) {  // all-gather of every rank's nonzero runs, summed in rank order
+                if (int rc = allgather(ctx, d.xg_send, d.xg_recv, (size_t)d.xg_P)) return rc;
+                LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_xunpack, dim3(blocks_for(d.nblk * 36 + d.nf * 6)), dim3(kBlock), 0, s, d));
+            } else {
+                COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);
+            }
         }
         if (!(d.fold && d.nch > 0))  // (folded into the last chunk of each block otherwise)
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_finalize, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
@@ -1421,7 +1514,7 @@ int graph_levels() {
 std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
     const Dev &d = ctx->d;
     return {d.E > 0, d.nf > 0, d.n_lm > 0, d.n > 0, d.nch > 0, d.band_mode, d.dense_mfma, d.dense_mfma ? d.ntiles : 0,
-            d.bw, d.bcr, d.cl, d.twisted, d.quad, d.sharded, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
+            d.bw, d.bcr, d.cl, d.twisted, d.quad, d.sharded, d.xg_P, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
             (int64_t)(getenv("PLBA_CHUNK_DIRECT") != nullptr), (int64_t)ctx->comm.kind};
 }
 int capture_step(plba_ctx *ctx) {
@@ -1504,6 +1597,16 @@ int agree_dev_error(plba_ctx *ctx, int mine, int *any) {
 
 // Run a schedule of 1 or 2 optimize() calls entirely on the device: replay the step graph in
 // batches, polling the control block once per batch.
+// every launch outside the step graphs is checked where it is issued (the graph launches are
+// checked by LAUNCH / launch_band)
+#define PLBA_LAUNCHED(ctx_, name_)                                                        \
+    do {                                                                                  \
+        const hipError_t le_ = hipGetLastError();                                         \
+        if (le_ != hipSuccess) {                                                          \
+            (ctx_)->set_error("kernel %s launch failed: %s", name_, hipGetErrorString(le_)); \
+            return PLBA_E_DEVICE;                                                         \
+        }                                                                                 \
+    } while (0)
 int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
     dev_error = false;
     Dev &d = ctx->d;
@@ -1511,7 +1614,7 @@ int run_schedule_once(plba_ctx *ctx, const Ctrl &init, bool &dev_error) {
     PLBA_CHECK(hipMemcpyAsync(d.ctrl, ctx->h_ctrl, sizeof(Ctrl), hipMemcpyHostToDevice, ctx->stream));
     if (d.n_ln > 0 && !init.hlm) {  // Plücker vectors of the current line states (read by k_linearize;
                                      // the hand-rolled LM starts from the map's NDw, uploaded instead)
-        hipLaunchKernelGGL(k_line_pluker, dim3(blocks_for(d.n_ln)), dim3(kBlock), 0, ctx->stream, d);
+        hipLaunchKernelGGL(k_line_pluker, dim3(blocks_for(d.n_ln)), dim3(kBlock), 0, ctx->stream, d); PLBA_LAUNCHED(ctx, "k_line_pluker");
         PLBA_CHECK(hipGetLastError());
     }
     // the host transport synchronises inside the step: no graph then
@@ -1651,7 +1754,7 @@ int do_optimize(plba_ctx *ctx, int iterations, int32_t *iters_done, double *fina
 }
 
 int launch_edges(plba_ctx *ctx, void (*k)(Dev, int), int arg) {
-    if (ctx->d.E > 0) hipLaunchKernelGGL(k, dim3(blocks_for(ctx->d.E)), dim3(kBlock), 0, ctx->stream, ctx->d, arg);
+    if (ctx->d.E > 0) hipLaunchKernelGGL(k, dim3(blocks_for(ctx->d.E)), dim3(kBlock), 0, ctx->stream, ctx->d, arg); PLBA_LAUNCHED(ctx, "edge kernel");
     PLBA_CHECK(hipGetLastError());
     return PLBA_OK;
 }
@@ -1662,9 +1765,9 @@ int gather_outputs(plba_ctx *ctx, std::vector<double> &out) {
     Dev &d = ctx->d;
     const size_t n = (size_t)d.n_lm_g * 4 + 3 * (size_t)d.E_g;
     PLBA_CHECK(hipMemsetAsync(d.gat, 0, n * sizeof(double), ctx->stream));
-    if (d.Ep) hipLaunchKernelGGL(k_depth, dim3(blocks_for(d.Ep)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth);
+    if (d.Ep) hipLaunchKernelGGL(k_depth, dim3(blocks_for(d.Ep)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth); PLBA_LAUNCHED(ctx, "k_depth");
     const int m = std::max(d.n_lm, d.E);
-    if (m) hipLaunchKernelGGL(k_gather, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth);
+    if (m) hipLaunchKernelGGL(k_gather, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d, ctx->d_depth); PLBA_LAUNCHED(ctx, "k_gather");
     PLBA_CHECK(hipGetLastError());
     int rc = allreduce(ctx, d.gat, d.gat, n);
     if (rc) return rc;
@@ -1696,7 +1799,7 @@ int download_outputs(plba_ctx *ctx, double *kf_Tcw, double *pt_xyz, double *ln_o
         ctx->h_out_cap = cap;
     }
     hipLaunchKernelGGL(k_out_scatter, dim3(blocks_for(m)), dim3(kBlock), 0, s, d, ctx->d_outd, ept_depth_ok ? 1 : 0,
-                       ctx->cur, ctx->chi_src);
+                       ctx->cur, ctx->chi_src); PLBA_LAUNCHED(ctx, "k_out_scatter");
     PLBA_CHECK(hipGetLastError());
     PLBA_CHECK(hipMemcpyAsync(ctx->h_out, ctx->d_outd, bytes, hipMemcpyDeviceToHost, s));
     PLBA_CHECK(hipStreamSynchronize(s));
@@ -2502,8 +2605,8 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
     const int eb = std::max((nact + kPgoNT - 1) / kPgoNT, 1);
     int cur = 0;
     // computeActiveErrors() after the initial guess
-    hipLaunchKernelGGL(k_pgo_linearize<false>, dim3(eb), dim3(kPgoNT), 0, s, P, cur);
-    hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 0, 0.0);
+    hipLaunchKernelGGL(k_pgo_linearize<false>, dim3(eb), dim3(kPgoNT), 0, s, P, cur); PLBA_LAUNCHED(ctx, "k_pgo_linearize");
+    hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 0, 0.0); PLBA_LAUNCHED(ctx, "k_pgo_sum");
     PLBA_CHECK(hipGetLastError());
     if (int rc = fetch()) return rc;
     res->chi2_initial = hout[0];
@@ -2513,11 +2616,11 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
     double lambda = 0.0, ni = 2.0, currentChi = hout[0];
     for (int it = 0; it < prm.max_iters && nfree > 0; ++it) {
         // OptimizationAlgorithmLevenberg::solve: computeActiveErrors, buildSystem
-        hipLaunchKernelGGL(k_pgo_linearize<true>, dim3(eb), dim3(kPgoNT), 0, s, P, cur);
-        hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 0, 0.0);
+        hipLaunchKernelGGL(k_pgo_linearize<true>, dim3(eb), dim3(kPgoNT), 0, s, P, cur); PLBA_LAUNCHED(ctx, "k_pgo_linearize");
+        hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 0, 0.0); PLBA_LAUNCHED(ctx, "k_pgo_sum");
         PLBA_CHECK(hipMemsetAsync(P.Hd, 0, sizeof(double) * (size_t)n * n, s));
-        hipLaunchKernelGGL(k_pgo_assemble, dim3((nblk * 42 + kPgoNT - 1) / kPgoNT), dim3(kPgoNT), 0, s, P);
-        if (it == 0 && prm.user_lambda_init <= 0.0) hipLaunchKernelGGL(k_pgo_maxdiag, dim3(1), dim3(64), 0, s, P);
+        hipLaunchKernelGGL(k_pgo_assemble, dim3((nblk * 42 + kPgoNT - 1) / kPgoNT), dim3(kPgoNT), 0, s, P); PLBA_LAUNCHED(ctx, "k_pgo_assemble");
+        if (it == 0 && prm.user_lambda_init <= 0.0) hipLaunchKernelGGL(k_pgo_maxdiag, dim3(1), dim3(64), 0, s, P); PLBA_LAUNCHED(ctx, "k_pgo_maxdiag");
         PLBA_CHECK(hipGetLastError());
         if (int rc = fetch()) return rc;
         currentChi = hout[0];
@@ -2531,19 +2634,19 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
         int qmax = 0;
         do {
             // setLambda + solve (dense LDLᵀ, Cholmod's positive-definite test) + update
-            hipLaunchKernelGGL(k_pgo_damp, dim3((unsigned)(((size_t)n * n + 255) / 256)), dim3(256), 0, s, P, Ad, lambda);
+            hipLaunchKernelGGL(k_pgo_damp, dim3((unsigned)(((size_t)n * n + 255) / 256)), dim3(256), 0, s, P, Ad, lambda); PLBA_LAUNCHED(ctx, "k_pgo_damp");
             for (int K = 0; K < ntiles; ++K) {  // the envelope's row tiles K..tl[K] only
                 const int m = tl[K] - K;
-                hipLaunchKernelGGL(k_dense_panel, dim3((m + 2) / 2), dim3(kDensePanelNT), 0, s, dd, K);
-                if (m > 0) hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, dd, K);
+                hipLaunchKernelGGL(k_dense_panel, dim3((m + 2) / 2), dim3(kDensePanelNT), 0, s, dd, K); PLBA_LAUNCHED(ctx, "k_dense_panel");
+                if (m > 0) hipLaunchKernelGGL(k_dense_update, dim3(m * (m + 1) / 2), dim3(64), 0, s, dd, K); PLBA_LAUNCHED(ctx, "k_dense_update");
             }
-            hipLaunchKernelGGL(k_pgo_check, dim3(1), dim3(256), 0, s, dd);
+            hipLaunchKernelGGL(k_pgo_check, dim3(1), dim3(256), 0, s, dd); PLBA_LAUNCHED(ctx, "k_pgo_check");
             hipLaunchKernelGGL(k_pgo_solve, dim3(1), dim3(kFacThreads),
-                               n <= dd.solve_lds_n ? sizeof(double) * (size_t)n : 0, s, dd);
-            hipLaunchKernelGGL(k_pgo_update, dim3((nv + kPgoNT - 1) / kPgoNT), dim3(kPgoNT), 0, s, P, cur);
+                               n <= dd.solve_lds_n ? sizeof(double) * (size_t)n : 0, s, dd); PLBA_LAUNCHED(ctx, "k_pgo_solve");
+            hipLaunchKernelGGL(k_pgo_update, dim3((nv + kPgoNT - 1) / kPgoNT), dim3(kPgoNT), 0, s, P, cur); PLBA_LAUNCHED(ctx, "k_pgo_update");
             // restoreDiagonal (Hd is untouched), computeActiveErrors at the trial state
-            hipLaunchKernelGGL(k_pgo_linearize<false>, dim3(eb), dim3(kPgoNT), 0, s, P, cur ^ 1);
-            hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 1, lambda);
+            hipLaunchKernelGGL(k_pgo_linearize<false>, dim3(eb), dim3(kPgoNT), 0, s, P, cur ^ 1); PLBA_LAUNCHED(ctx, "k_pgo_linearize");
+            hipLaunchKernelGGL(k_pgo_sum, dim3(1), dim3(64), 0, s, P, (const Ctrl *)ctrl_d, 1, lambda); PLBA_LAUNCHED(ctx, "k_pgo_sum");
             PLBA_CHECK(hipGetLastError());
             if (int rc = fetch()) return rc;
             const bool ok = hout[3] != 0.0;

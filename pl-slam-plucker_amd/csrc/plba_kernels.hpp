@@ -173,10 +173,22 @@ struct Dev {
     int32_t n_lm_g, E_g;                // whole-window landmark / edge counts
     // Out-of-place (send *_loc -> receive) so that replaying a step whose kernels were guarded
     // off re-reduces unchanged partials and leaves the totals intact.
-    double *red_iter, *red_iter_loc;    // [nf*43 + 2 + nranks]: Hpp | b_p | #active edges | χ² | active | lm max per rank
+    double *red_iter, *red_iter_loc;    // [nf*43 + 2 + nranks] (sharded [nf*13 + ...], see Hdg): Hpp | b_p | #active edges | χ² | active | lm max per rank
     double *red_rcs, *red_rcs_loc;      // [nblk*36 + nf*6]: Σ A₁ᵀZ₁Z₂ᵀA₂ per block | Σ A_eᵀq_e per pose
+    // sharded, all-gather exchange (xg_P > 0): each rank's partial RCS is nonzero only on the
+    // block rows of its keyframe range; xg_rng[4r..4r+3] = rank r's two runs of red_rcs
+    // (block run start, length | right-hand-side run start, length, in doubles), xg_send = this
+    // rank's runs packed (P doubles; host transport: its slot of an R x P array), xg_recv = R x P
+    double *xg_send, *xg_recv;
+    int64_t *xg_rng;
+    int64_t xg_P;
+    int32_t xg_host;
     double *red_dec, *red_dec_loc;      // [2]: trial χ² | landmark part of Σx(λx+b)
     double *Hpp_w, *bp_w;               // where pose_combine writes (== Hpp, bp unless sharded)
+    // sharded: the iteration all-reduce carries only diag(Hpp) | b_p | active counts | scalars
+    // (nf·13 + 2 + R); this rank's full partial Hpp (Hpp_w, local) rides in the RCS exchange inside
+    // its diagonal blocks (k_rcs_blockpart), so Hpp is nullptr and Hdg holds the summed diagonals
+    double *Hdg, *Hdg_w;                // [nf][6] (sharded only)
     double *pose_part;                  // [nf][kPoseParts][kPP] partial Σ AᵀA (upper), Σ Aᵀc, #active edges
     double *pact, *pact_w;              // [nf] active edges of each free pose (0 = vertex inactive in g2o)
     int32_t *lm_gpos, *e_gpos;          // local landmark / edge -> whole-window position
@@ -672,6 +684,7 @@ __device__ __forceinline__ double pose_partial(const Dev &d, int h, int part) {
                 const int cc = r + rem;
                 d.Hpp_w[(size_t)h * 36 + r * 6 + cc] = v;
                 d.Hpp_w[(size_t)h * 36 + cc * 6 + r] = v;
+                if (r == cc && d.Hdg_w) d.Hdg_w[(size_t)h * 6 + r] = v;
                 if (r != cc) v = 0.0;
             } else if (k < 27) {
                 d.bp_w[(size_t)h * 6 + (k - 21)] = v;
@@ -816,7 +829,7 @@ __global__ __launch_bounds__(kInitNT) void k_iter_pack(Dev d) {
     int any = 0;
     for (int i = threadIdx.x; i < d.n_lm_blocks; i += kInitNT) any |= d.part_any[i];
     any = __syncthreads_or(any);
-    double *o = d.red_iter_loc + (size_t)d.nf * 43;
+    double *o = d.red_iter_loc + (size_t)d.nf * 13;  // (sharded layout: diag | b_p | active | scalars)
     if (threadIdx.x == 0) {
         o[0] = chi;
         o[1] = any ? 1.0 : 0.0;
@@ -833,9 +846,9 @@ __device__ __forceinline__ void iter_init_body(const Dev &d, double *sh) {
     double chi, mx;
     bool any;
     if (d.sharded) {  // totals from the all-reduced iteration array
-        const double *o = d.red_iter + (size_t)d.nf * 43;
+        const double *o = d.red_iter + (size_t)d.nf * 13;
         double m = 0.0;
-        for (int i = threadIdx.x; i < d.nf * 6; i += NT) m = fmax(m, fabs(d.Hpp[(i / 6) * 36 + (i % 6) * 7]));
+        for (int i = threadIdx.x; i < d.nf * 6; i += NT) m = fmax(m, fabs(d.Hdg[i]));
         for (int r = threadIdx.x; r < d.nranks; r += NT) m = fmax(m, o[2 + r]);
         mx = block_max<NT>(m, sh);
         chi = o[0];
@@ -1024,12 +1037,16 @@ __device__ __forceinline__ void rcs_finalize_entry(const Dev &d, int b, int e, d
     }
     const int r = e / 6, c = e % 6;
     if (diag) {
-        double h = d.Hpp[(size_t)i1 * 36 + e] - sacc;
+        // (sharded: the exchanged sum already holds −Hpp, k_rcs_blockpart)
+        double h = (d.Hpp ? d.Hpp[(size_t)i1 * 36 + e] : 0.0) - sacc;
         // a free pose with no active edge is not in g2o's system (SparseOptimizer activation,
         // SURVEY.md §8 A13); its all-zero block row becomes I (x = 0 exactly) instead of λI,
         // which would be a zero pivot at λ = 0
         // (hand-rolled LM: Marquardt damping H(i,i) += λ·H(i,i), src/mapHandler.cpp:2114-2115)
-        if (r == c) h += d.pact[i1] == 0.0 ? 1.0 : d.ctrl->hlm ? d.lam * d.Hpp[(size_t)i1 * 36 + e] : d.lam;
+        if (r == c)
+            h += d.pact[i1] == 0.0 ? 1.0
+                 : d.ctrl->hlm   ? d.lam * (d.Hpp ? d.Hpp[(size_t)i1 * 36 + e] : d.Hdg[(size_t)i1 * 6 + r])
+                                 : d.lam;
         if (d.band_mode) d.Bd[((size_t)i1 * (d.bw + 1)) * 36 + e] = h;
         else d.Ad[(size_t)(6 * i1 + r) + (size_t)(6 * i1 + c) * n] = h;
         if (d.twisted) d.Bd2[((size_t)(d.nf - 1 - i1) * (d.bw + 1)) * 36 + e] = h;
@@ -1209,8 +1226,35 @@ __global__ __launch_bounds__(kBlock) void k_rcs_blockpart(Dev d0) {
     if (e >= 36 && i1 != d.blk_i2[b]) return;
     double sacc = 0.0;
     for (int c = d.blk_ch[b]; c < d.blk_ch[b + 1]; ++c) sacc += d.ch_part[(size_t)c * 42 + e];
-    if (e < 36) d.red_rcs_loc[(size_t)b * 36 + e] = sacc;
-    else d.red_rcs_loc[(size_t)d.nblk * 36 + 6 * i1 + (e - 36)] = sacc;
+    // this rank's partial Hpp into its diagonal blocks (the sum is S − Hpp: rcs_finalize_entry)
+    if (e < 36 && i1 == d.blk_i2[b]) sacc -= d.Hpp_w[(size_t)i1 * 36 + e];
+    const int64_t x = e < 36 ? (int64_t)b * 36 + e : (int64_t)d.nblk * 36 + 6 * i1 + (e - 36);
+    if (d.xg_P > 0) {  // packed into this rank's all-gather record (outside its runs: zero by construction)
+        const int64_t *rg = d.xg_rng + 4 * (size_t)d.rank;
+        int64_t o;
+        if (x >= rg[0] && x < rg[0] + rg[1]) o = x - rg[0];
+        else if (x >= rg[2] && x < rg[2] + rg[3]) o = rg[1] + (x - rg[2]);
+        else return;
+        d.xg_send[(d.xg_host ? (size_t)d.rank * d.xg_P : 0) + o] = sacc;
+    } else {
+        d.red_rcs_loc[x] = sacc;
+    }
+}
+
+// sharded pass 2b (all-gather exchange): the full red_rcs as the sum, in rank order, of every
+// rank's runs — the same additions on every rank, so every rank factorises the same matrix
+__global__ __launch_bounds__(kBlock) void k_rcs_xunpack(Dev d0) {
+    TRIAL_SLOT(0)
+    const int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (x >= (int64_t)d.nblk * 36 + (int64_t)d.nf * 6) return;
+    double s = 0.0;
+    for (int r = 0; r < d.nranks; ++r) {
+        const int64_t *rg = d.xg_rng + 4 * (size_t)r;
+        const double *rv = d.xg_recv + (size_t)r * d.xg_P;
+        if (x >= rg[0] && x < rg[0] + rg[1]) s += rv[x - rg[0]];
+        else if (x >= rg[2] && x < rg[2] + rg[3]) s += rv[rg[1] + (x - rg[2])];
+    }
+    d.red_rcs[x] = s;
 }
 
 // pass 2: per block entry, sum its chunks in order, add Hpp + λI (diagonal), write the band /

@@ -133,3 +133,34 @@ def test_gba_matches_oracle(solver, cfg, params):
     solver.upload(win.graph)
     out = solver.hlm_lba(win, p)
     _compare(out, ref, win)
+
+
+def test_gba_c5_bounded_matches_oracle_fixture(solver):
+    """GBA at its natural size: the C5 window, max_iters = 2, against the oracle's
+    result committed by tools/make_gba_fixture.py (refhlm takes ~100 s per run at C5, so the
+    fixture holds the counters, trace, every pose and a seeded sample of 4000 points / 1000 lines)."""
+    import os
+    from plba.hlm import gba_window
+    path = os.path.join(os.path.dirname(__file__), "golden", "gba_C5_it2.npz")
+    with np.load(path, allow_pickle=False) as z:
+        ref = dict(z)
+    win = gba_window(synth.generate("C5"))
+    solver.upload(win.graph)
+    out = solver.hlm_lba(win, capi.gba_params(max_iters=2))
+    assert [out["linearizations"], out["solves"], out["accepted"]] == list(ref["counters"])
+    tg = out["trace"]
+    np.testing.assert_array_equal(tg["iter"], ref["trace_int"][:, 0])
+    np.testing.assert_array_equal(tg["result"], ref["trace_int"][:, 1])
+    np.testing.assert_allclose(tg["lambda_start"], ref["trace_lam"][:, 0], rtol=1e-9)
+    np.testing.assert_allclose(tg["lambda_end"], ref["trace_lam"][:, 1], rtol=1e-9)
+    assert out["err"] == ref["err"][0] or (np.isnan(out["err"]) and np.isnan(ref["err"][0]))
+    assert out["dx_norm"] == pytest.approx(ref["err"][1], rel=1e-4, abs=1e-30)
+    np.testing.assert_allclose(out["kf_x"], ref["kf_x"], rtol=0, atol=1e-6)
+
+    def close(a, b, x0, key):
+        tol = 1e-4 * np.abs(b - x0).max() + 1e-12 * max(np.abs(b).max(), 1.0)
+        assert np.abs(a - b).max() <= tol, (key, np.abs(a - b).max(), tol)
+
+    close(out["kf_Tcw"], ref["kf_Tcw"], ref["init_kf_Tcw"], "kf_Tcw")
+    close(np.asarray(out["pt_xyz"]).reshape(-1, 3)[ref["pt_idx"]], ref["pt_xyz"], ref["init_pt"], "pt_xyz")
+    close(np.asarray(out["ln_line3d"]).reshape(-1, 6)[ref["ln_idx"]], ref["ln_line3d"], ref["init_ln"], "ln_line3d")
