@@ -144,7 +144,7 @@ int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on);   /* HIP-event timing 
  * a step evaluates at most (speculative damped trials, 1 = off), [18]=their policy
  * (0 off, 1 always, 2 after a rejection in the iteration, 3 after the first rejection of the
  * optimize() call), [19]=device steps the last schedule took, [20]=four-segment column-lane
- * factorisation (1/0).
+ * factorisation (1/0), [21]=window structure built on the device (1) or on the host (0).
  * Counts are this rank's when the window is sharded. */
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap);
 int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,

@@ -121,6 +121,7 @@ struct plba_ctx {
     // context to the column-lane factorisation for good (no_bcr) and solve the window again
     bool no_bcr = false;
     int bcr_fallbacks = 0;
+    int dev_build = 0;  // the last upload's window structure was built on the device
     int fb_cl = 0, fb_twisted = 0, fb_tw_m = 0;  // the factorisation the window falls back to
     double *bk_T = nullptr, *bk_X = nullptr, *bk_xp = nullptr, *bk_xk = nullptr, *bk_Lpb = nullptr, *bk_XL = nullptr,
            *bk_xl = nullptr;
@@ -533,25 +534,40 @@ std::vector<int32_t> rcm_from_adj(std::vector<std::vector<int32_t>> &adj);
 // doubles of the download staging block before its byte outputs
 inline size_t out_doubles(size_t n_kf, size_t n_pt, size_t n_ln, size_t E) { return n_kf * 12 + n_pt * 3 + n_ln * 4 + E; }
 std::vector<int32_t> rcm_order(const plba_graph *g, const std::vector<int32_t> &kf_hidx, int nf) {
-    const int nl = g->n_pt + g->n_ln;
-    std::vector<std::vector<int32_t>> lm_poses(nl);
+    // landmark -> free poses as a CSR (counting sort of the edges by landmark), then the coupling
+    // graph as an nf x nf bit matrix: its rows are the sorted, duplicate-free adjacency lists
+    const int np_ = g->n_pt, nl = np_ + g->n_ln;
+    std::vector<int32_t> off(nl + 1, 0);
+    for (int e = 0; e < g->n_ept; ++e) off[g->ept_lm[e] + 1] += kf_hidx[g->ept_kf[e]] >= 0;
+    for (int e = 0; e < g->n_eln; ++e) off[np_ + g->eln_lm[e] + 1] += kf_hidx[g->eln_kf[e]] >= 0;
+    for (int l = 0; l < nl; ++l) off[l + 1] += off[l];
+    std::vector<int32_t> fill(off.begin(), off.end() - 1), hs(off[nl]);
     for (int e = 0; e < g->n_ept; ++e) {
         const int h = kf_hidx[g->ept_kf[e]];
-        if (h >= 0) lm_poses[g->ept_lm[e]].push_back(h);
+        if (h >= 0) hs[fill[g->ept_lm[e]]++] = h;
     }
     for (int e = 0; e < g->n_eln; ++e) {
         const int h = kf_hidx[g->eln_kf[e]];
-        if (h >= 0) lm_poses[g->n_pt + g->eln_lm[e]].push_back(h);
+        if (h >= 0) hs[fill[np_ + g->eln_lm[e]]++] = h;
     }
-    std::vector<std::vector<int32_t>> adj(nf);
-    for (auto &v : lm_poses) {
-        std::sort(v.begin(), v.end());
-        v.erase(std::unique(v.begin(), v.end()), v.end());
-        for (size_t i = 0; i < v.size(); ++i)
-            for (size_t j = i + 1; j < v.size(); ++j) {
-                adj[v[i]].push_back(v[j]);
-                adj[v[j]].push_back(v[i]);
+    const size_t W = ((size_t)nf + 63) / 64;
+    std::vector<uint64_t> bits((size_t)nf * W, 0);
+    for (int l = 0; l < nl; ++l)
+        for (int i = off[l]; i < off[l + 1]; ++i)
+            for (int j = i + 1; j < off[l + 1]; ++j) {
+                const int a = hs[i], b = hs[j];
+                if (a == b) continue;
+                bits[(size_t)a * W + b / 64] |= 1ull << (b % 64);
+                bits[(size_t)b * W + a / 64] |= 1ull << (a % 64);
             }
+    std::vector<std::vector<int32_t>> adj(nf);
+    for (int h = 0; h < nf; ++h) {
+        const uint64_t *row = bits.data() + (size_t)h * W;
+        int cnt = 0;
+        for (size_t w = 0; w < W; ++w) cnt += __builtin_popcountll(row[w]);
+        adj[h].reserve(cnt);
+        for (size_t w = 0; w < W; ++w)
+            for (uint64_t m = row[w]; m; m &= m - 1) adj[h].push_back((int32_t)(w * 64 + __builtin_ctzll(m)));
     }
     return rcm_from_adj(adj);
 }
@@ -715,8 +731,33 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         }
         first_blk = wb.first_blk;
         for (int h = 0; h < nf; ++h) bw = std::max(bw, h - first_blk[h]);
-        // an envelope the banded kernels cannot take may narrow under the RCM order: host build
-        devb = !(bw > kClMaxBW && nf > 2 && !env_flag("PLBA_NO_RCM"));
+        // an envelope the banded kernels cannot take may narrow under the RCM order (the host
+        // build's rule, same permutation: rcm_order over the whole graph): build again with the
+        // reordered free poses, kept when the envelope narrows, else built once more in id order
+        if (bw > kClMaxBW && nf > 2 && !env_flag("PLBA_NO_RCM")) {
+            const std::vector<int32_t> rcm = rcm_order(g, kf_hidx, nf);
+            std::vector<int32_t> pos(nf), h2(n_kf, -1);
+            for (int i = 0; i < nf; ++i) pos[rcm[i]] = i;
+            for (int k = 0; k < n_kf; ++k) h2[k] = kf_hidx[k] >= 0 ? pos[kf_hidx[k]] : -1;
+            wb.kf_hidx = h2.data();
+            int brc2 = build_stage1(ctx->bmemA, wb, msg, sizeof msg);
+            int bw2 = 0;
+            for (int h = 0; h < nf && !brc2; ++h) bw2 = std::max(bw2, h - wb.first_blk[h]);
+            if (!brc2 && bw2 < bw) {
+                kf_hidx = h2;
+                first_blk = wb.first_blk;
+                bw = bw2;
+            } else {
+                wb.kf_hidx = kf_hidx.data();
+                if (!brc2) brc2 = build_stage1(ctx->bmemA, wb, msg, sizeof msg);
+            }
+            if (brc2) {
+                ctx->set_error("%s", msg);
+                return brc2;
+            }
+            mark("device build (RCM order)");
+        }
+        devb = true;
         if (devb) {
             n_pt = wb.n_pt; n_ln = wb.n_ln; Ep = wb.Ep; El = wb.El;
             ctx->n_free_edges = wb.n_free_edges;
@@ -737,6 +778,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         }
         mark("device build (stage 1)");
     }
+    ctx->dev_build = devb ? 1 : 0;
     if (!devb) {
     // landmarks owned by this rank (all of them unless the window is sharded)
     std::vector<int32_t> pt_owner(n_pt_g, 0), ln_owner(n_ln_g, 0);
@@ -2208,12 +2250,12 @@ int plba_debug_bcr_stamps(plba_ctx *ctx, unsigned long long *out, int32_t cap, i
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
     if (!ctx || !out) return PLBA_E_INVALID;
     if (!ctx->uploaded) return PLBA_E_STATE;
-    const int64_t v[21] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
+    const int64_t v[22] = {ctx->d.nf, ctx->d.bw, ctx->d.nblk, (int64_t)ctx->n_triples, ctx->d.E, ctx->d.n_lm,
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
                            ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N,
                            ctx->d.dense_mfma, ctx->bcr_fallbacks, ctx->d.spec_max, ctx->d.spec_policy,
-                           ctx->h_ctrl ? ctx->h_ctrl->steps : 0, ctx->d.quad};
-    for (int i = 0; i < cap && i < 21; ++i) out[i] = v[i];
+                           ctx->h_ctrl ? ctx->h_ctrl->steps : 0, ctx->d.quad, ctx->dev_build};
+    for (int i = 0; i < cap && i < 22; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

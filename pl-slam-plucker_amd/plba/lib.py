@@ -287,13 +287,13 @@ class Solver:
         return {names[i].decode(): (float(ms[i]), int(nl[i])) for i in range(n.value)}
 
     def structure_stats(self) -> dict:
-        st = (C.c_int64 * 21)()
-        self._check(self.L.plba_structure_stats(self.ctx, st, 21), "plba_structure_stats")
+        st = (C.c_int64 * 22)()
+        self._check(self.L.plba_structure_stats(self.ctx, st, 22), "plba_structure_stats")
         return dict(nf=st[0], bw=st[1], nblk=st[2], triples=st[3], edges=st[4], landmarks=st[5], banded=st[6],
                     chunks=st[7], free_edges=st[8], point_edges=st[9], graph=st[10], sharded=st[11],
                     twisted=st[12], column_lane=st[13], bcr_rows=st[14], dense_mfma=st[15],
                     bcr_fallbacks=st[16], spec_slots=st[17], spec_policy=st[18], device_steps=st[19],
-                    quad=st[20])
+                    quad=st[20], device_build=st[21])
 
     def synchronize(self):
         self._check(self.L.plba_synchronize(self.ctx), "plba_synchronize")

@@ -70,6 +70,35 @@ def test_device_build_equals_host_build(monkeypatch, case):
         assert np.array_equal(out_d[k], out_h[k]), k
 
 
+def _scrambled_ids(g, seed=11):
+    h = g.copy()
+    h.kf_id = np.random.default_rng(seed).permutation(g.n_kf).astype(np.int32)
+    return h
+
+
+RCM_CASES = {
+    "C2R": lambda: synth.generate("C2R"),
+    "C3R": lambda: synth.generate("C3R"),
+    "C2_scrambled": lambda: _scrambled_ids(synth.generate("C2")),
+    "C1L_scrambled": lambda: _scrambled_ids(synth.generate("C1L", n_kf=40, n_pt=800, n_ln=160, seed=43)),
+}
+
+
+@pytest.mark.parametrize("case", list(RCM_CASES))
+def test_device_build_rcm_equals_host_build(monkeypatch, case):
+    """Windows whose id-order envelope is too wide for the banded kernels (a revisit loop,
+    scrambled keyframe ids): the device build reorders the free poses by the host build's RCM
+    permutation and builds again on the device — same structure, bitwise-equal solves."""
+    g = RCM_CASES[case]()
+    st_d, out_d = _solve(monkeypatch, g, host=False)
+    st_h, out_h = _solve(monkeypatch, g, host=True)
+    assert st_d["device_build"] == 1 and st_h["device_build"] == 0, (st_d, st_h)
+    for k in STRUCT:
+        assert st_d[k] == st_h[k], (k, st_d, st_h)
+    for k in KEYS:
+        assert np.array_equal(out_d[k], out_h[k]), k
+
+
 def test_device_build_invalid_edge_reported(monkeypatch):
     from plba.lib import PlbaError, Solver
     g = synth.generate("C1L")
