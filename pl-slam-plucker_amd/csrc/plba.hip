@@ -1426,11 +1426,21 @@ int allgather(plba_ctx *ctx, const double *send, double *recv, size_t P) {
         if (_rc) return _rc;                                 \
     } while (0)
 
+// Schur assembly with two lanes per triple (k_rcs_chunk_h) once a slot's chunk waves exceed what
+// k_rcs_chunk keeps resident (1.75 waves per SIMD x 1024 SIMDs) — per slot, so that the choice
+// (and the rounding) does not depend on the trial-slot count; PLBA_CHUNK_HALF_MIN overrides the
+// threshold (0: always, a huge value: never)
+bool chunk_half(const Dev &d) {
+    const char *e = getenv("PLBA_CHUNK_HALF_MIN");  // (read per capture: tests switch it)
+    const long long thr = e ? atoll(e) : 1792LL;
+    return (long long)d.nch > thr;
+}
 int launch_step(plba_ctx *ctx) {
     Dev &d = ctx->d;
     hipStream_t s = ctx->stream;
     // PLBA_CHUNK_DIRECT=1: per-lane A/Z row loads in the Schur assembly (A/B of the staged copy)
     static const bool chunk_direct = getenv("PLBA_CHUNK_DIRECT") != nullptr;
+
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     if (d.nf > 0 || d.n_lm > 0) {
         const int nred = kPoseParts * d.nf + (d.n_lm > 0 ? d.n_lm_blocks : 0);
@@ -1448,7 +1458,7 @@ int launch_step(plba_ctx *ctx) {
     }
     if (d.n > 0) {
         if (!d.band_mode) LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
-        if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(chunk_direct ? k_rcs_chunk<false> : k_rcs_chunk<true>, dim3(8 * ((d.nch + 7) / 8), d.spec_max), dim3(64), 0, s, d));
+        if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(chunk_direct ? k_rcs_chunk<false> : chunk_half(d) ? k_rcs_chunk_h : k_rcs_chunk<true>, dim3(8 * ((d.nch + 7) / 8), d.spec_max), dim3(64), 0, s, d));
         if (d.sharded) {
             LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
             if (d.xg_P > 0) {  // all-gather of every rank's nonzero runs, summed in rank order
@@ -1557,7 +1567,7 @@ std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
     const Dev &d = ctx->d;
     return {d.E > 0, d.nf > 0, d.n_lm > 0, d.n > 0, d.nch > 0, d.band_mode, d.dense_mfma, d.dense_mfma ? d.ntiles : 0,
             d.bw, d.bcr, d.cl, d.twisted, d.quad, d.sharded, d.xg_P, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
-            (int64_t)(getenv("PLBA_CHUNK_DIRECT") != nullptr), (int64_t)ctx->comm.kind};
+            (int64_t)(getenv("PLBA_CHUNK_DIRECT") != nullptr), (int64_t)chunk_half(d), (int64_t)ctx->comm.kind};
 }
 int capture_step(plba_ctx *ctx) {
     if (ctx->step_exec && !ctx->graphs_stale) return PLBA_OK;

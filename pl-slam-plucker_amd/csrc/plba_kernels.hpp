@@ -1216,6 +1216,164 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d0) {
     }
 }
 
+// Chunked reduced-camera assembly with two lanes per triple, for windows with more chunks than
+// k_rcs_chunk's waves can hold at once (chunk_half_min, plba.hip): lane h·32 + p takes triple p
+// of a 32-triple batch and accumulates block rows 3h .. 3h+2 of A₁ᵀ(Z₁Z₂ᵀ)A₂ (18) and of A_eᵀq_e
+// (3). Half the accumulators and half the staging per wave: 216 → 146 VGPRs and 22 → 11 KB of LDS,
+// 3 waves per SIMD instead of 1.75 to hide the row loads, at twice the batches per wave (so a
+// window whose chunks all fit at once keeps k_rcs_chunk: C3 24.9 vs 25.3 µs; C5 121.7 → 114.7 µs).
+// The per-element sums run over the same triples in another lane partition (deterministic, not
+// bitwise equal to k_rcs_chunk's).
+#ifndef PLBA_CHH_MINB
+#define PLBA_CHH_MINB 3  // waves per SIMD the register budget is sized for (4 spills: 115 -> 226 us at C5)
+#endif
+__global__ __launch_bounds__(64, PLBA_CHH_MINB) void k_rcs_chunk_h(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
+    constexpr int NB = 32, NA = 22;  // triples per batch; accumulators per lane (21) padded
+    __shared__ double smem[64 * NA];  // staging: A₁ | A₂ (32x12) | Z₁ | Z₂ (32x8); then red[64][NA]
+    double(*red)[NA] = reinterpret_cast<double(*)[NA]>(smem);
+    // XCD-aware chunk order (as k_rcs_chunk)
+    const int nb = d.nch, per = (nb + 7) / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int full = nb - 8 * (per - 1);
+    if (xcd >= full && slot >= per - 1) return;  // padding
+    const int ch = xcd < full ? xcd * per + slot : full * per + (xcd - full) * (per - 1) + slot;
+    const int lane = threadIdx.x, p = lane & (NB - 1), h = lane >> 5;
+    const bool hlm = d.ctrl->hlm != 0;
+    const int b = d.ch_blk[ch];
+    const bool diag = d.blk_i1[b] == d.blk_i2[b];
+    double acc[21];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) acc[k] = 0.0;
+    const int t0 = d.ch_off[ch], t1 = d.ch_off[ch + 1];
+    int2 nx = make_int2(0, 0);
+    if (t0 < t1) nx = reinterpret_cast<const int2 *>(d.trip)[min(t0 + p, t1 - 1)];
+    dbl2 *sA1 = reinterpret_cast<dbl2 *>(smem), *sA2 = sA1 + NB * 6;
+    dbl2 *sZ1 = sA2 + NB * 6, *sZ2 = sZ1 + NB * 4;
+#pragma unroll 1
+    for (int q = 0; q < kChunk / NB; ++q) {
+        const int tb = t0 + NB * q;
+        if (tb >= t1) break;  // wave-uniform
+        const int t = tb + p;
+        const int e1 = nx.x, e2 = nx.y;
+        if (tb + NB < t1) nx = reinterpret_cast<const int2 *>(d.trip)[min(tb + NB + p, t1 - 1)];
+        // cooperative row loads: A pieces 64j + lane of the batch's 32 x 6, Z pieces of 32 x 4
+        dbl2 v1[3], v2[3], w1[2], w2[2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int pc = 64 * j + lane, r = pc / 6, k = pc - 6 * r;
+            const int f1 = __shfl(e1, r, 64), f2 = __shfl(e2, r, 64);
+            v1[j] = reinterpret_cast<const dbl2 *>(d.A + (size_t)f1 * 12)[k];
+            v2[j] = reinterpret_cast<const dbl2 *>(d.A + (size_t)f2 * 12)[k];
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = 16 * j + (lane >> 2), k = lane & 3;
+            const int f1 = __shfl(e1, r, 64), f2 = __shfl(e2, r, 64);
+            w1[j] = reinterpret_cast<const dbl2 *>(d.Z + (size_t)f1 * 8)[k];
+            w2[j] = reinterpret_cast<const dbl2 *>(d.Z + (size_t)f2 * 8)[k];
+        }
+        __syncthreads();  // the previous batch's rows are read
+        // bank-conflict-free reads as k_rcs_chunk (rotated Z stores, rotated A reads)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) { sA1[64 * j + lane] = v1[j]; sA2[64 * j + lane] = v2[j]; }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = 16 * j + (lane >> 2), k = lane & 3, pos = 4 * r + ((k + ((r >> 2) & 3)) & 3);
+            sZ1[pos] = w1[j];
+            sZ2[pos] = w2[j];
+        }
+        __syncthreads();
+        double m00 = 0, m01 = 0, m10 = 0, m11 = 0;
+        {
+            const int rz = (p >> 2) & 3;
+            double z1[8], z2[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int pos = 4 * p + ((k + rz) & 3);
+                const dbl2 x = sZ1[pos], y = sZ2[pos];
+                z1[2 * k] = x.x; z1[2 * k + 1] = x.y; z2[2 * k] = y.x; z2[2 * k + 1] = y.y;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                m00 = fma(z1[k], z2[k], m00);
+                m01 = fma(z1[k], z2[4 + k], m01);
+                m10 = fma(z1[4 + k], z2[k], m10);
+                m11 = fma(z1[4 + k], z2[4 + k], m11);
+            }
+        }
+        if (hlm) m00 += m11;  // (as k_rcs_chunk)
+        // Q = (Z₁Z₂ᵀ) A₂ from the A₂ row (read rotated as k_rcs_chunk), then this lane's A₁
+        // entries 3h .. 3h+2 of both residual rows (pieces 3h/2, 3h/2 + 1 and 3 + the same)
+        const int ra = (p >> 3) & 1;
+        double Q[12];
+        {
+            dbl2 tA2[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) tA2[k] = sA2[6 * p + (k + ra < 6 ? k + ra : k + ra - 6)];
+            double a2[12];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const dbl2 y = ra ? tA2[(k + 5) % 6] : tA2[k];
+                a2[2 * k] = y.x; a2[2 * k + 1] = y.y;
+            }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                Q[k] = m00 * a2[k] + m01 * a2[6 + k];
+                Q[6 + k] = m10 * a2[k] + m11 * a2[6 + k];
+            }
+        }
+        double a1[6];
+        {
+            const int k0 = h;  // pieces h, h+1 hold entries 2h .. 2h+3 ⊇ 3h .. 3h+2
+            const dbl2 x0 = sA1[6 * p + k0], x1 = sA1[6 * p + k0 + 1];
+            const dbl2 y0 = sA1[6 * p + 3 + k0], y1 = sA1[6 * p + 4 + k0];
+            // h = 0: (x0.x, x0.y, x1.x); h = 1: (x0.y, x1.x, x1.y) — entries 3h + rr = 2h + (h + rr)
+            a1[0] = h ? x0.y : x0.x;
+            a1[1] = h ? x1.x : x0.y;
+            a1[2] = h ? x1.y : x1.x;
+            a1[3] = h ? y0.y : y0.x;
+            a1[4] = h ? y1.x : y0.y;
+            a1[5] = h ? y1.y : y1.x;
+        }
+        if (t < t1) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) acc[r * 6 + c] += a1[r] * Q[c] + a1[3 + r] * Q[6 + c];
+            if (diag && e1 == e2) {
+                const double q0 = d.q[(size_t)e1 * 2], q1 = d.q[(size_t)e1 * 2 + 1];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) acc[18 + r] += a1[r] * q0 + a1[3 + r] * q1;
+            }
+        }
+    }
+    __syncthreads();  // the staging rows are read before red overwrites them
+#pragma unroll
+    for (int k = 0; k < 21; ++k) red[lane][k] = acc[k];
+    __syncthreads();
+    if (lane < 42) {
+        // entry (r, c) of the block (lane < 36) or row r of the right-hand side (36..41): the 32
+        // lanes of half r / 3, in lane order
+        const int r = lane < 36 ? lane / 6 : lane - 36, hh = r / 3;
+        const int k = lane < 36 ? (r % 3) * 6 + lane % 6 : 18 + r % 3;
+        double sacc = 0.0;
+        for (int l = 0; l < NB; ++l) sacc += red[hh * NB + l][k];
+        st_sc1(d.ch_part + (size_t)ch * 42 + lane, sacc);
+    }
+    if (d.fold && arrive_last(d.cnt_rcs + b, d.blk_ch[b + 1] - d.blk_ch[b]) && lane < 42) {
+        double sacc = 0.0;
+        const int c1 = d.blk_ch[b + 1];
+        for (int c0 = d.blk_ch[b]; c0 < c1; c0 += 4) {  // 4 partials in flight, summed in chunk order
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = c0 + u < c1 ? ld_sc1(d.ch_part + (size_t)(c0 + u) * 42 + lane) : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sacc += v[u];
+        }
+        rcs_finalize_entry(d, b, lane, sacc);
+    }
+}
+
 // sharded pass 2a: this rank's per-block sums (chunks in order) into the all-reduced array
 __global__ __launch_bounds__(kBlock) void k_rcs_blockpart(Dev d0) {
     TRIAL_SLOT(0)

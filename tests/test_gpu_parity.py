@@ -57,3 +57,26 @@ def test_rerun_is_bitwise_deterministic(solver):
     b = solver.lba_plucker()
     for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2"):
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("cfg", ["C1L", "C2", "C3"])
+@pytest.mark.parametrize("half", ["0", "1000000000"], ids=["two-lanes", "one-lane"])
+def test_schur_assembly_variants_match_oracle(monkeypatch, cfg, half):
+    """Both reduced-camera assembly kernels on every window size: k_rcs_chunk_h (two lanes per
+    triple, chosen by default only above PLBA_CHUNK_HALF_MIN chunk waves) and k_rcs_chunk (one lane
+    per triple) — oracle parity and bitwise-deterministic reruns."""
+    from plba.lib import Solver
+    monkeypatch.setenv("PLBA_CHUNK_HALF_MIN", half)
+    g = synth.generate(cfg)
+    ref = oa.lba_plucker(g)
+    with Solver() as s:
+        s.upload(g)
+        out = s.lba_plucker()
+        s.reset()
+        again = s.lba_plucker()
+    m = compare(out, ref)
+    assert m["pt_level_diff"] == 0 and m["ln_level_diff"] == 0, m
+    assert_parity(m)
+    np.testing.assert_array_equal(out["iters"], ref["iters"])
+    for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2"):
+        assert np.array_equal(out[k], again[k]), k
