@@ -2569,7 +2569,12 @@ constexpr int kLmsNT = 256;  // k_lm_solve workgroup: 64 landmarks
 // longer tracks fall back to a loop for the remainder. Every load of the kernel that does not
 // depend on another load is issued up front, so a landmark costs two dependent global round
 // trips (CSR offsets -> edge records, then x_p / trial poses) instead of one per phase.
-constexpr int kLmSlots = 2;
+// (one slot: 2 → 1 cut the kernel's registers enough for 3 waves per SIMD; C5 94.7 → 89 µs,
+// C3 unchanged; the edges of a lane are visited in the same order either way)
+#ifndef PLBA_LM_SLOTS
+#define PLBA_LM_SLOTS 1
+#endif
+constexpr int kLmSlots = PLBA_LM_SLOTS;
 struct LmEdge {
     int e, h, kf;
     bool act;
@@ -2803,7 +2808,11 @@ __global__ __launch_bounds__(kBlock) void k_decide(Dev d) {
     decide_body<kBlock>(d, sh);
 }
 
+#ifdef PLBA_LM_WPE
+__global__ __launch_bounds__(kLmsNT, PLBA_LM_WPE) void k_lm_solve(Dev d0) {
+#else
 __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
+#endif
     TRIAL_SLOT(blockIdx.y)
     __shared__ double sh[kLmsNT / 64];
     const int nslots = d0.ctrl->spec_w;  // (read before this workgroup arrives: k_decide changes it)
