@@ -584,7 +584,10 @@ __global__ __launch_bounds__(kBlock) void k_linearize(Dev d) {
 //     as one 256-thread workgroup per pose, so the sums are deterministic;
 //   workgroups [kPoseParts·nf, ...): 64 landmarks each, Hll = Σ B_eᵀB_e, b_l = Σ B_eᵀc_e
 //     (and, on a stage switch, the landmark activation).
-constexpr int kPoseParts = 4;
+#ifndef PLBA_POSE_PARTS
+#define PLBA_POSE_PARTS 4
+#endif
+constexpr int kPoseParts = PLBA_POSE_PARTS;
 #ifndef PLBA_POSE_KU
 #define PLBA_POSE_KU 4  // pose-part edges with loads in flight per pass
 #endif
