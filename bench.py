@@ -426,8 +426,6 @@ def main():
         if name == "k_rcs_factor" and info.get("banded"):
             if info.get("bcr_rows"):
                 prof_name = "k_rcs_factor_bcr"
-            elif info.get("quad"):
-                prof_name = "k_rcs_factor_quad_cl"
             else:
                 prof_name = "k_rcs_factor_twisted" if info.get("twisted") else "k_rcs_factor_band"
                 if info.get("column_lane"):
@@ -437,11 +435,7 @@ def main():
         chain = None
         if name == "k_rcs_factor" and info.get("banded") and not info.get("bcr_rows"):
             nf_, bw_ = int(info["nf"]), int(info["bw"])
-            if info.get("quad"):
-                L4 = nf_ - 3 * bw_
-                seg = max((L4 + 3) // 4, (L4 - (L4 + 3) // 4 + 1) // 2)
-                chain = 2 * (seg + 2 * bw_)
-            elif info.get("twisted"):
+            if info.get("twisted"):
                 chain = 2 * ((nf_ - bw_ + 1) // 2 + bw_)
             else:
                 chain = 2 * nf_
@@ -493,8 +487,7 @@ def main():
                 "upload_ms": upload_ms,
                 "end_to_end": e2e[-1],
                 "factorisation": ("block cyclic reduction over %d super-rows" % info["bcr_rows"] if info.get("bcr_rows")
-                                  else ("four-segment column-lane band LDLT" if info.get("quad")
-                                        else ("two-sided column-lane band LDLT" if info.get("twisted") else "band LDLT"))),
+                                  else ("two-sided column-lane band LDLT" if info.get("twisted") else "band LDLT")),
                 "speculative_trials": {"slots": info.get("spec_slots", 1), "policy": info.get("spec_policy", 0),
                                        "device_steps_per_lba": info.get("device_steps")},
                 "parallelism": (f"landmark-sharded window over {world} GPU(s)" if shard

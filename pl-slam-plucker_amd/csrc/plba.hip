@@ -340,33 +340,6 @@ const void *cl_kernel_impl(int bw, bool twisted, std::integer_sequence<int, B...
      ...);
     return k;
 }
-template <int... B>
-const void *quad_kernel_impl(int bw, std::integer_sequence<int, B...>) {
-    const void *k = nullptr;
-    ((bw == B ? (k = (const void *)k_rcs_factor_quad_cl<B>, 0) : 0), ...);
-    return k;
-}
-inline const void *quad_kernel(int bw) { return quad_kernel_impl(bw, std::make_integer_sequence<int, kQuadMaxBW + 1>{}); }
-inline size_t quad_lds_bytes(int bw, int nf) { return sizeof(double) * quad_lds_doubles(bw, nf); }
-// Four-segment split (plba_band_quad.hpp): segment lengths n1 (Seg1), n2, n3 (the middle segments,
-// >= bw so that the separators do not couple), n4 (Seg4) of nf - 3·bw rows; false when the window is
-// too short for it to shorten the two-sided chain ((nf + bw)/2 steps against ~(nf - 3bw)/4 + 2bw)
-// or its LDS does not fit. PLBA_QUAD=0 disables (A/B runs).
-inline bool quad_split(int nf, int bw, int &n1, int &n2, int &n3, int &n4) {
-    const char *e = getenv("PLBA_QUAD");
-    if (!(e && e[0] == '1')) return false;  // opt-in while it is being measured
-    if (bw < 2 || bw > kQuadMaxBW || quad_lds_bytes(bw, nf) > 159 * 1024) return false;
-    const int L = nf - 3 * bw;
-    n1 = (L + 3) / 4;
-    n4 = (L - n1 + 2) / 3;
-    n2 = (L - n1 - n4 + 1) / 2;
-    n3 = L - n1 - n4 - n2;
-    if (n1 < 1 || n4 < 1 || n2 < bw || n3 < bw) return false;
-    // latency model: the middle segments' spike sweeps cost about one extra step per 4, the two extra
-    // hand-offs ~4 steps; the two-sided chain is (nf + bw)/2 + ~4 (one hand-off)
-    const double t_quad = n2 * 1.25 + 2.0 * bw + 8.0, t_tw = (nf + bw) / 2.0 + 4.0;
-    return (e && e[0] == '1') || t_quad < t_tw;
-}
 // column-lane factorisation (plba_band_cl.hpp) for bandwidths up to kClMaxBW
 inline bool use_cl(int bw) {
     const char *f = getenv("PLBA_FACTOR");
@@ -471,8 +444,6 @@ inline hipError_t launch_band(Dev &d, hipStream_t s) {
         if (e != hipSuccess) return e;
         return hipLaunchKernel(bcr_back_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrBackNT), args, bcr_back_lds_bytes(d.bw), s);
     }
-    if (d.quad)
-        return hipLaunchKernel(quad_kernel(d.bw), dim3(4, d.spec_max), dim3(kClNT), args, quad_lds_bytes(d.bw, d.nf), s);
     if (d.cl) {
         const void *k = cl_kernel_impl(d.bw, d.twisted != 0, std::make_integer_sequence<int, kClMaxBW + 1>{});
         return hipLaunchKernel(k, dim3(d.twisted ? 2 : 1, d.spec_max), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
@@ -745,6 +716,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             for (int h = 0; h < nf && !brc2; ++h) bw2 = std::max(bw2, h - wb.first_blk[h]);
             if (!brc2 && bw2 < bw) {
                 kf_hidx = h2;
+                wb.kf_hidx = kf_hidx.data();  // (h2 dies with this block)
                 first_blk = wb.first_blk;
                 bw = bw2;
             } else {
@@ -1059,14 +1031,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.cl = cl && cl_lds_bytes(bw, nf, twisted) <= 159 * 1024 ? 1 : 0;
     d.twisted = twisted ? 1 : 0;
     d.tw_m = twisted ? tw_split(nf, bw) : 0;
-    {  // four segments instead of two (same reversed band arrays as the two-sided kernel)
-        int n1 = 0, n2 = 0, n3 = 0, n4 = 0;
-        d.quad = d.cl && twisted && quad_split(nf, bw, n1, n2, n3, n4) ? 1 : 0;
-        d.q_a = d.quad ? n1 : 0;
-        d.q_p = d.quad ? n1 + bw + n2 : 0;
-        d.q_n3 = d.quad ? n3 : 0;
-        d.q_n4 = d.quad ? n4 : 0;
-    }
     d.corrected = ctx->opts.corrected_line_jacobian;
     // Speculative trials: worth it where the step is bound by the serial factorisation
     // chain and the rest of the chip idles during it — the column-lane factorisation (one or two
@@ -1230,11 +1194,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ZALLOC(d.tw_fail, 2 * (size_t)W);
         ZALLOC(d.tw_count, (size_t)W);
     }
-    if (d.quad) {
-        ALLOC(d.qbuf, (size_t)W * quad_buf_doubles(bw, nf));
-        ZALLOC(d.qcnt, 3 * (size_t)W);
-        ZALLOC(d.qfail, 6 * (size_t)W);
-    }
     if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate
         ALLOC(d.bcr_pub, (size_t)d.bcr_N * bcr_pub_doubles(bw));
         ALLOC(d.bcr_x, (size_t)d.bcr_N * bcr_xrec(bw));
@@ -1351,8 +1310,6 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, false)));
         }
     }
-    if (d.quad)
-        PLBA_CHECK(hipFuncSetAttribute(quad_kernel(bw), hipFuncAttributeMaxDynamicSharedMemorySize, (int)quad_lds_bytes(bw, nf)));
     if (d.cl) {  // the column-lane kernel's LDS grows with nf (x_p staging of the two-sided variant)
         const void *k = cl_kernel_impl(bw, twisted, std::make_integer_sequence<int, kClMaxBW + 1>{});
         PLBA_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cl_lds_bytes(bw, nf, twisted)));
@@ -1571,7 +1528,7 @@ int graph_levels() {
 std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
     const Dev &d = ctx->d;
     return {d.E > 0, d.nf > 0, d.n_lm > 0, d.n > 0, d.nch > 0, d.band_mode, d.dense_mfma, d.dense_mfma ? d.ntiles : 0,
-            d.bw, d.bcr, d.cl, d.twisted, d.quad, d.sharded, d.xg_P, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
+            d.bw, d.bcr, d.cl, d.twisted, d.sharded, d.xg_P, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
             (int64_t)(getenv("PLBA_CHUNK_DIRECT") != nullptr), (int64_t)chunk_half(d), (int64_t)ctx->comm.kind};
 }
 int capture_step(plba_ctx *ctx) {
@@ -2269,7 +2226,7 @@ int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
                            ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N,
                            ctx->d.dense_mfma, ctx->bcr_fallbacks, ctx->d.spec_max, ctx->d.spec_policy,
-                           ctx->h_ctrl ? ctx->h_ctrl->steps : 0, ctx->d.quad, ctx->dev_build};
+                           ctx->h_ctrl ? ctx->h_ctrl->steps : 0, 0, ctx->dev_build};  // [20]: unused (was the four-segment flag)
     for (int i = 0; i < cap && i < 22; ++i) out[i] = v[i];
     return PLBA_OK;
 }

@@ -136,14 +136,7 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #pragma unroll
                     for (int r = 0; r < 6; ++r) pA[cs * 36 + cc * 6 + r] = v[r];
                 }
-#ifdef PLBA_CL_SYNC
-                wave_lds_sync();
-#endif
                 double a1[36];
-#ifdef PLBA_CL_NOA1  // timing experiment only: wrong results
-#pragma unroll
-                for (int q = 0; q < 36; ++q) a1[q] = 1e-3 * q;
-#endif
                 STAMP(0);
                 // B: Gauss–Jordan on block row k across the lanes (pivot lanes 6*sk + p)
 #pragma unroll
@@ -153,23 +146,17 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #pragma unroll
                     for (int r = 0; r < 6; ++r) f[r] = readlane_f64(v[r], pl);
                     if (f[p] == 0.0) fail = true;
-#ifdef PLBA_CL_NR2
-                    const double rp = rcp_nr(f[p]);
-#else
                     const double rp = rcp_nr1(f[p]);
-#endif
                     const double mp = v[p] * rp;
 #pragma unroll
                     for (int r = 0; r < 6; ++r) v[r] = r == p ? mp : fma(-f[r], mp, v[r]);
                 }
-#ifndef PLBA_CL_NOA1
                 // A_{k+1,k} only feeds E/F: read after the Gauss–Jordan, so B does not wait for
                 // 18 broadcast reads (C and the barrier cover their latency; the sched_barrier
                 // keeps the scheduler from sinking them to their use): step 2,696 -> 2,570 cycles
 #pragma unroll
                 for (int q = 0; q < 36; ++q) a1[q] = pA[s1 * 36 + q];
                 __builtin_amdgcn_sched_barrier(0);
-#endif
                 STAMP(1);
                 // C: publish X_i = L_{i,k}ᵀ (lane 6s+c holds row c of L_{i,k}) and z_k
                 if (clane && cs != sk) {
@@ -214,9 +201,6 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
             } else {
                 lds_barrier();
                 STAMP(3);
-#ifdef PLBA_CL_NOWORK
-                if (k >= 0) { sk = s1; lk = l1; continue; }  // timing experiment only: wrong results
-#endif
                 // block row k+2+bw enters slot lk (row k is consumed)
                 if (wt < NROW) {
                     const double val = k + 2 + BW < nrows ? wpf[u] : 0.0;

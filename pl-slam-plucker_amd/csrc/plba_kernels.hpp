@@ -201,11 +201,6 @@ struct Dev {
     double *Lband2, *Kinv2, *zb2;       // factors of the bottom segment (reversed numbering)
     double *tw_sep;                     // [2][bw][bw+1][36] + [2][bw][6] separator windows
     int32_t *tw_fail, *tw_count;        // [2] per-segment failure, arrival counter
-    // four-segment factorisation (plba_band_quad.hpp): Seg1 [0, q_a), S1, Seg2, S2 from q_p, Seg3 of
-    // q_n3 rows, S3, Seg4 of q_n4 rows (natural numbering)
-    int32_t quad, q_a, q_p, q_n3, q_n4;
-    double *qbuf;                       // [quad_buf_doubles] hand-off record
-    int32_t *qcnt, *qfail;              // [3] arrival counters, [6] failure flags
     // block cyclic reduction over super-rows of bw pose blocks (plba_bcr.hpp)
     int32_t bcr, bcr_N;                 // enabled; super-rows (= workgroups of the launch)
     double *bcr_pub;                    // [N][bcr_pub_doubles(bw)] Schur contributions + coupling
@@ -233,13 +228,6 @@ __host__ __device__ __forceinline__ size_t sl_sep(const Dev &d) {
 }
 __host__ __device__ __forceinline__ size_t sl_chp(const Dev &d) { return (size_t)(d.nch > 1 ? d.nch : 1) * 42; }
 __host__ __device__ __forceinline__ size_t sl_lms(const Dev &d) { return (size_t)(d.n_lms_blocks > 1 ? d.n_lms_blocks : 1); }
-// hand-off record of the four-segment factorisation (plba_band_quad.hpp): 4 separator windows,
-// 2 spike couplings, 4 spike Schur terms, 4 rhs terms, G of the two middle segments and of the
-// two outer separators
-__host__ __device__ __forceinline__ size_t quad_buf_doubles(int bw, int nf) {
-    const size_t NS = 6 * (size_t)bw, QW = (size_t)bw * (bw + 1) * 36 + (size_t)bw * 6;
-    return 4 * QW + 2 * (size_t)bw * 6 * NS + 4 * NS * NS + 4 * NS + 2 * (size_t)nf * 6 * NS + 2 * (size_t)bw * 6 * NS;
-}
 
 // The window as trial slot s sees it: λ_s (g2o's λ after s rejections: λ *= ν, ν *= 2 — the same
 // operations in the same order, so bitwise the λ the sequential loop would use), the state it
@@ -286,11 +274,6 @@ __device__ __forceinline__ Dev slot_view(const Dev &d0, int s) {
             d.tw_sep += ss * sl_sep(d0);
             d.tw_fail += 2 * ss;
             d.tw_count += ss;
-        }
-        if (d0.quad) {
-            d.qbuf += ss * quad_buf_doubles(d0.bw, d0.nf);
-            d.qcnt += 3 * ss;
-            d.qfail += 6 * ss;
         }
         d.part_lm += ss * sl_lms(d0);
         d.part_lms += ss * sl_lms(d0);
@@ -2345,7 +2328,6 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d0) {
 }
 
 #include "plba_band_cl.hpp"
-#include "plba_band_quad.hpp"
 #include "plba_bcr.hpp"
 #include "plba_dense.hpp"
 #include "plba_pgo.hpp"
@@ -2816,9 +2798,19 @@ __global__ __launch_bounds__(kLmsNT, PLBA_LM_WPE) void k_lm_solve(Dev d0) {
 #else
 __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
 #endif
-    TRIAL_SLOT(blockIdx.y)
+    // Not TRIAL_SLOT: the folded decision (last arriver) rewrites Ctrl::spec_w inside this launch,
+    // so a workgroup dispatched after it would read the NEXT step's width. Every workgroup of the
+    // grid (gridDim.y = spec_max) therefore arrives, idle slots included, and all of them read
+    // spec_w before arriving: the arrival total does not depend on spec_w and no workgroup can
+    // observe the decision's writes.
+    TRIAL_GUARD_OF(d0)
     __shared__ double sh[kLmsNT / 64];
-    const int nslots = d0.ctrl->spec_w;  // (read before this workgroup arrives: k_decide changes it)
+    const int nslots = d0.ctrl->spec_w;
+    if ((int)blockIdx.y >= nslots) {
+        if (d0.fold && arrive_last(d0.cnt, (int32_t)(gridDim.x * gridDim.y))) decide_body<kLmsNT>(d0, sh);
+        return;
+    }
+    const Dev d = slot_view(d0, (int)blockIdx.y);
     const int gt = blockIdx.x * kLmsNT + threadIdx.x;
     const int l = gt / kLmLanes, q = gt % kLmLanes;   // a quad never straddles a wave
     const bool live = l < d.n_lm;
@@ -3050,7 +3042,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
         st_sc1(d.part_lm + blockIdx.x, s1);
     }
     // the last workgroup to finish takes the trial decision (k_decide's work)
-    if (d.fold && arrive_last(d.cnt, (int32_t)gridDim.x * nslots)) decide_body<kLmsNT>(d0, sh);
+    if (d.fold && arrive_last(d.cnt, (int32_t)(gridDim.x * gridDim.y))) decide_body<kLmsNT>(d0, sh);
 }
 // sharded: this rank's trial χ² and landmark scale terms into the all-reduced decision array
 __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {

@@ -414,28 +414,3 @@ def test_bcr_residency_limit_selects_column_lane(monkeypatch, solver):
     st = solver.structure_stats()
     assert st["bcr_rows"] == 0 and st["column_lane"] == 1, st
     _check(solver.lba_plucker(), oa.lba_plucker(g))
-
-
-@pytest.mark.parametrize("tmax", [2, 3, 5, 8])
-def test_four_segment_factorisation_bandwidths(solver, monkeypatch, tmax):
-    """Four-segment column-lane LDLᵀ (plba_band_quad.hpp: two spike sweeps, three separators) at
-    bandwidths 1..7 on 96-KF windows, against the oracle and against the two-sided kernel (another
-    elimination order of the same exact LDLᵀ: equal to rounding)."""
-    g = synth.generate("C1L", n_kf=96, n_pt=30 * 96, n_ln=6 * 96, seed=700 + tmax, track_min=2, track_max=tmax,
-                       fixed_frac=0.1)
-    ref = oa.lba_plucker(g)
-    monkeypatch.setenv("PLBA_QUAD", "1")
-    solver.upload(g)
-    st = solver.structure_stats()
-    if not 2 <= st["bw"] <= 7:
-        pytest.skip(f"bandwidth {st['bw']} outside 2..7: no four-segment split")
-    assert st["quad"] == 1 and st["twisted"] == 1 and st["column_lane"] == 1, st
-    quad = solver.lba_plucker()
-    _check(quad, ref)
-    monkeypatch.setenv("PLBA_QUAD", "0")
-    solver.upload(g)
-    assert solver.structure_stats()["quad"] == 0
-    two = solver.lba_plucker()
-    monkeypatch.delenv("PLBA_QUAD")
-    assert np.abs(quad["kf_Tcw"] - two["kf_Tcw"]).max() < 1e-9
-    assert np.abs(quad["pt_xyz"] - two["pt_xyz"]).max() < 1e-7 * max(1.0, np.abs(two["pt_xyz"]).max())

@@ -90,8 +90,8 @@ def test_speculative_slots_are_bitwise_the_sequential_solve(cfg):
 def test_speculative_failed_solves_follow_the_sequential_loop(cfg):
     """Solves forced to fail by a deterministic function of λ (PLBA_DIAG bit 128): a failed trial is
     rejected and applies the last successful solve's x (A13); a slot failing after an earlier
-    slot of the same step succeeded is evaluated again alone. Bitwise the one-slot run (C2: the
-    two-sided factorisation, C3: the four-segment one)."""
+    slot of the same step succeeded is evaluated again alone. Bitwise the one-slot run (C2 and C3:
+    the two-sided column-lane factorisation)."""
     g = synth.generate(cfg)
     base, _, _ = _solve(g, 1, 0, diag=128)
     assert any(t["trials"] > 1 for t in base["trace"]), base["trace"]
@@ -99,6 +99,23 @@ def test_speculative_failed_solves_follow_the_sequential_loop(cfg):
         out, out2, _ = _solve(g, slots, pol, diag=128)
         _assert_same(base, out, (slots, pol))
         _assert_same(base, out2, (slots, pol, "second schedule"))
+
+
+def test_speculative_slot_width_changes_on_an_oversubscribed_grid():
+    """The folded decision (last k_lm_solve workgroup) changes the next step's slot count inside
+    the launch. With far more k_lm_solve workgroups than the device holds at once (C4: ~1.5k per
+    slot), late workgroups of the idle slot run after the decision: they must neither run as a live
+    slot nor skew the arrival count. The sticky policy goes 1 -> 2 slots at the first
+    rejection; the result must stay bitwise the one-slot solve, twice in a row."""
+    g = synth.generate("C4")
+    with _Env(PLBA_FACTOR="cl"):
+        base, _, st0 = _solve(g, 1, 0)
+        assert st0["column_lane"] == 1 and st0["bcr_rows"] == 0, st0
+        for slots, pol in ((2, 3), (3, 2)):
+            out, out2, st = _solve(g, slots, pol)
+            assert st["spec_slots"] == slots, st
+            _assert_same(base, out, (slots, pol))
+            _assert_same(base, out2, (slots, pol, "second schedule"))
 
 
 def test_speculative_zero_pivot_window():
