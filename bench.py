@@ -217,6 +217,24 @@ def relaunch_distributed(a) -> int:
     return subprocess.run(cmd).returncode
 
 
+# Per-step phase split of a (sharded) window from one kernel-timed LBA (DESIGN §7's model):
+# work every rank does on its own landmark share, work every rank repeats on the whole reduced
+# camera system, and the collectives between them.
+SHARDED_KERNELS = ("k_linearize", "k_iter_reduce", "k_edge_schur", "k_rcs_chunk", "k_lm_solve", "k_shard_pack")
+
+
+def phases(ktimes: dict, steps: int) -> dict:
+    st = max(int(steps or 0), 1)
+    sh = sum(ms for k, (ms, n) in ktimes.items() if k in SHARDED_KERNELS)
+    co = sum(ms for k, (ms, n) in ktimes.items() if k == "collectives")
+    rep = sum(ms for k, (ms, n) in ktimes.items() if k not in SHARDED_KERNELS and k != "collectives")
+    return {"device_steps_per_lba": st, "sharded_us_per_step": sh * 1e3 / st,
+            "replicated_us_per_step": rep * 1e3 / st, "collective_us_per_step": co * 1e3 / st,
+            "note": "event-timed kernels of one instrumented LBA: sharded = per-rank edge/landmark work "
+                    "(divides by N), replicated = factorisation + init/finalize/decide (every rank), "
+                    "collective = the exchanges (host transport: incl. the host round trip)"}
+
+
 def shard_child(a, world: int):
     """Rank 0 of a replicas job with N > 1: the sharded C5 strong-scaling job on the same N GPUs,
     as a child process group (its own torch.distributed.run), after the replicas measurement. A
@@ -326,6 +344,7 @@ def main():
     ktimes = s.kernel_times()
     info = s.structure_stats()
     s.L.plba_enable_kernel_timing(s.ctx, 0)
+    ph = phases(ktimes, info.get("device_steps")) if shard else None
 
     s.synchronize()
     if dist is not None:
@@ -390,10 +409,14 @@ def main():
                 ri += int(rr["iters"][0] + rr["iters"][1])
             ref.synchronize()
             rdt = time.perf_counter() - t0
+            ref.L.plba_enable_kernel_timing(ref.ctx, 1)
+            ref.reset()
+            ref.lba_plucker(want_outputs=False, with_trace=False)
+            ref_ph = phases(ref.kernel_times(), ref.structure_stats().get("device_steps"))
             ref.close()
             scaling_ref = {"config": a.config, "n_gpus": 1, "mode": "the same window, unsharded, one GPU",
                            "value": ri / rdt, "unit": "LM iterations/s", "steps": a.steps,
-                           "speedup_of_this_run": (tot_iters / dt) / (ri / rdt)}
+                           "speedup_of_this_run": (tot_iters / dt) / (ri / rdt), "phases": ref_ph}
         dist.barrier()
 
     hmirror = None
@@ -481,6 +504,10 @@ def main():
                             f"{g.n_ln} Plücker lines, {g.n_ept}+{g.n_eln} edges; "
                             + (f"one window sharded over {world} GPU(s) by landmark ({a.transport} all-reduce)"
                                if shard else "one independent window per GPU"),
+                "edges": int(g.n_ept + g.n_eln),
+                # SURVEY.md §8d sizes the configs at 5 observations per landmark; the generator's
+                # visibility rejection leaves ~4.7 (C3: 112,416 of the nominal 120,000 edges)
+                "survey_nominal_edges": int(5 * (g.n_pt + g.n_ln)),
                 "lm_iterations_per_lba": it_per_lba,
                 "trials_per_lba": trials / a.steps,
                 "ms_per_lm_iteration": dt / max(iters, 1) * 1e3,
@@ -520,6 +547,8 @@ def main():
             "kernels": per_kernel,
         }
         out["final_chi2_gpu"] = [float(r["chi2"][0]), float(r["chi2"][1])]
+        if ph is not None:
+            out["phases"] = ph
         if scaling_ref is not None:
             out["scaling_reference"] = scaling_ref
         if shard_run is not None:

@@ -43,12 +43,15 @@ namespace plba {
 
 enum KernelId {
     K_LINEARIZE, K_REDUCE, K_ITER_INIT, K_ESCHUR, K_MEMSET, K_ASSEMBLE, K_FINALIZE, K_FACTOR,
-    K_POSE_UPDATE, K_LM_UPDATE, K_EVAL, K_DECIDE, K_DENSE_PANEL, K_DENSE_UPDATE, K_COUNT
+    K_POSE_UPDATE, K_LM_UPDATE, K_EVAL, K_DECIDE, K_DENSE_PANEL, K_DENSE_UPDATE,
+    K_PACK,  // sharded: this rank's partials packed for an exchange (per-rank work)
+    K_COMM,  // sharded: the collectives themselves (RCCL, or the host transport's round trip)
+    K_COUNT
 };
 static const char *kKernelNames[K_COUNT] = {
     "k_linearize", "k_iter_reduce", "k_iter_init", "k_edge_schur", "memset_rcs",
     "k_rcs_chunk", "k_rcs_finalize", "k_rcs_factor", "k_pose_update", "k_lm_solve", "k_edge_eval", "k_decide",
-    "k_dense_panel", "k_dense_update"};
+    "k_dense_panel", "k_dense_update", "k_shard_pack", "collectives"};
 
 }  // namespace plba
 
@@ -1382,10 +1385,11 @@ int allgather(plba_ctx *ctx, const double *send, double *recv, size_t P) {
     }
     return allreduce(ctx, send, recv, (size_t)c.nranks * P);
 }
-#define COMM(send, recv, n)                                  \
-    do {                                                     \
-        int _rc = allreduce(ctx, (send), (recv), (size_t)(n)); \
-        if (_rc) return _rc;                                 \
+#define COMM(send, recv, n)                                                        \
+    do {                                                                           \
+        int _crc = 0;                                                              \
+        LAUNCH(K_COMM, _crc = allreduce(ctx, (send), (recv), (size_t)(n)));        \
+        if (_crc) return _crc;                                                     \
     } while (0)
 
 // Schur assembly with two lanes per triple (k_rcs_chunk_h) once a slot's chunk waves exceed what
@@ -1409,7 +1413,7 @@ int launch_step(plba_ctx *ctx) {
         LAUNCH(K_REDUCE, hipLaunchKernelGGL(k_iter_reduce, dim3(nred), dim3(kLmBlock), 0, s, d));
     }
     if (d.sharded) {
-        LAUNCH(K_ITER_INIT, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kInitNT), 0, s, d));
+        LAUNCH(K_PACK, hipLaunchKernelGGL(k_iter_pack, dim3(1), dim3(kInitNT), 0, s, d));
         COMM(d.red_iter_loc, d.red_iter, (size_t)d.nf * 13 + 2 + d.nranks);
     }
     const bool reduced = d.nf > 0 || d.n_lm > 0;
@@ -1422,9 +1426,11 @@ int launch_step(plba_ctx *ctx) {
         if (!d.band_mode) LAUNCH(K_MEMSET, (void)hipMemsetAsync(d.Ad, 0, sizeof(double) * (size_t)d.n * d.n, s));
         if (d.nch > 0) LAUNCH(K_ASSEMBLE, hipLaunchKernelGGL(chunk_direct ? k_rcs_chunk<false> : chunk_half(d) ? k_rcs_chunk_h : k_rcs_chunk<true>, dim3(8 * ((d.nch + 7) / 8), d.spec_max), dim3(64), 0, s, d));
         if (d.sharded) {
-            LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
+            LAUNCH(K_PACK, hipLaunchKernelGGL(k_rcs_blockpart, dim3(blocks_for(d.nblk * 42)), dim3(kBlock), 0, s, d));
             if (d.xg_P > 0) {  // all-gather of every rank's nonzero runs, summed in rank order
-                if (int rc = allgather(ctx, d.xg_send, d.xg_recv, (size_t)d.xg_P)) return rc;
+                int grc = 0;
+                LAUNCH(K_COMM, grc = allgather(ctx, d.xg_send, d.xg_recv, (size_t)d.xg_P));
+                if (grc) return grc;
                 LAUNCH(K_FINALIZE, hipLaunchKernelGGL(k_rcs_xunpack, dim3(blocks_for(d.nblk * 36 + d.nf * 6)), dim3(kBlock), 0, s, d));
             } else {
                 COMM(d.red_rcs_loc, d.red_rcs, (size_t)d.nblk * 36 + (size_t)d.nf * 6);
@@ -1459,7 +1465,7 @@ int launch_step(plba_ctx *ctx) {
         LAUNCH(K_LM_UPDATE, hipLaunchKernelGGL(k_lm_solve, dim3(d.n_lms_blocks, d.spec_max), dim3(kLmsNT), 0, s, d));
     }
     if (d.sharded) {
-        LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide_pack, dim3(1), dim3(kBlock), 0, s, d));
+        LAUNCH(K_PACK, hipLaunchKernelGGL(k_decide_pack, dim3(1), dim3(kBlock), 0, s, d));
         COMM(d.red_dec_loc, d.red_dec, 2);
     }
     if (!(d.fold && d.n_lm > 0))  // (folded into the last k_lm_solve workgroup otherwise)

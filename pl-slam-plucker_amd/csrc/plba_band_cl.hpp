@@ -41,6 +41,42 @@ __device__ __forceinline__ double rcp_nr1(double x) {
     return fma(fma(-x, r, 1.0), r, r);
 }
 
+// Lane-local LDLᵀ of a 6x6 symmetric block held as its packed lower triangle (row-major,
+// ltri(i, j) for j <= i): on return s holds the unit lower factor below the diagonal and dv the
+// reciprocal pivots. zp is set if a pivot is exactly zero (SimplicialLDLT's failure condition).
+__host__ __device__ constexpr int ltri(int i, int j) { return i * (i + 1) / 2 + j; }
+__device__ __forceinline__ void ldl6_inplace(double (&s)[21], double (&dv)[6], bool &zp) {
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+        const double dp = s[ltri(p, p)];
+        zp = zp || dp == 0.0;
+        const double rp = rcp_nr1(dp);
+        dv[p] = rp;
+        double col[6];
+#pragma unroll
+        for (int i = p + 1; i < 6; ++i) col[i] = s[ltri(i, p)];
+#pragma unroll
+        for (int i = p + 1; i < 6; ++i) s[ltri(i, p)] = col[i] * rp;
+#pragma unroll
+        for (int i = p + 1; i < 6; ++i)
+#pragma unroll
+            for (int j = p + 1; j <= i; ++j) s[ltri(i, j)] = fma(-s[ltri(i, p)], col[j], s[ltri(i, j)]);
+    }
+}
+// x <- (L D Lᵀ)⁻¹ x with the factors of ldl6_inplace
+__device__ __forceinline__ void ldl6_solve(const double (&s)[21], const double (&dv)[6], double (&x)[6]) {
+#pragma unroll
+    for (int i = 1; i < 6; ++i)
+#pragma unroll
+        for (int m = 0; m < i; ++m) x[i] = fma(-s[ltri(i, m)], x[m], x[i]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] *= dv[i];
+#pragma unroll
+    for (int i = 4; i >= 0; --i)
+#pragma unroll
+        for (int m = 5; m > i; --m) x[i] = fma(-s[ltri(m, i)], x[m], x[i]);
+}
+
 // Eliminates block rows k0..k1-1 of an nrows-row band (g.nrows). The LDS window (row i in slot
 // i mod (bw+2), block (i, i-w) row-major) is loaded for rows k0..k0+bw+1 when load_window is
 // set, otherwise it is taken as left by a previous call (plus whatever the caller added to it).
@@ -138,6 +174,22 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
                 }
                 double a1[36];
                 STAMP(0);
+#ifdef PLBA_CL_LL
+                // B': every lane factors S_k = A_{k,k} (the pivot group's published columns) in its
+                // own registers and applies S_k⁻¹ to its own column: no cross-lane dependency
+                {
+                    double s[21], dv[6];
+                    const double *Sk = pA + sk * 36;  // entry (r, c) at [c * 6 + r]
+#pragma unroll
+                    for (int i = 0; i < 6; ++i)
+#pragma unroll
+                        for (int j = 0; j <= i; ++j) s[ltri(i, j)] = Sk[j * 6 + i];
+                    bool zp = false;
+                    ldl6_inplace(s, dv, zp);
+                    if (zp) fail = true;
+                    ldl6_solve(s, dv, v);
+                }
+#else
                 // B: Gauss–Jordan on block row k across the lanes (pivot lanes 6*sk + p)
 #pragma unroll
                 for (int p = 0; p < 6; ++p) {
@@ -151,6 +203,7 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
 #pragma unroll
                     for (int r = 0; r < 6; ++r) v[r] = r == p ? mp : fma(-f[r], mp, v[r]);
                 }
+#endif
                 // A_{k+1,k} only feeds E/F: read after the Gauss–Jordan, so B does not wait for
                 // 18 broadcast reads (C and the barrier cover their latency; the sched_barrier
                 // keeps the scheduler from sinking them to their use): step 2,696 -> 2,570 cycles

@@ -44,7 +44,7 @@ def load(path: Optional[str] = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("PLBA_LIB") or LIB_PATH  # (PLBA_LIB: A/B builds of the same library)
     if not os.path.exists(path):
         raise PlbaError(f"libplba.so not found at {path}: run `make -C pl-slam-plucker_amd` "
                         "(or __graft_entry__.build()) first")

@@ -81,10 +81,11 @@ def plan_and_schur_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def sharded_gpu_worker(rank, world, port, outdir, cfg, transport, host_build=False):
+def sharded_gpu_worker(rank, world, port, outdir, cfg, transport, host_build=False, own_device=False):
     """GPU rank (all ranks may share one GPU with the host transport): full sharded LBA.
     host_build: PLBA_HOST_BUILD=1 (the host window build and its shard_plan) instead of the device
-    build's own ownership kernel (k_b_owner)."""
+    build's own ownership kernel (k_b_owner). own_device: rank r on GPU r (one process per GPU,
+    the RCCL transport's deployment)."""
     if host_build:
         os.environ["PLBA_HOST_BUILD"] = "1"
     dist = init_gloo(rank, world, port)
@@ -95,7 +96,7 @@ def sharded_gpu_worker(rank, world, port, outdir, cfg, transport, host_build=Fal
     po, lo = shard_plan(g, world)  # the documented plan (plba_shard_plan)
     plan_lm = int((po == rank).sum() + (lo == rank).sum())
     plan_e = int((po[g.ept_lm] == rank).sum() + (lo[g.eln_lm] == rank).sum())
-    s = sharded_solver(device=0, transport=transport)
+    s = sharded_solver(device=rank if own_device else 0, transport=transport)
     s.upload(g)
     out = s.lba_plucker()
     s.reset()

@@ -1,8 +1,9 @@
 """Sharded windows on the GPU against the CPU oracle.
 
 Two ranks share the box's one GPU through the host transport (gloo all-reduces); a 1-rank
-RCCL communicator exercises the RCCL transport and its capture into the step graph. The
-multi-GPU RCCL run itself is the driver's scaling bench (`bench.py --mode shard`)."""
+RCCL communicator exercises the RCCL transport and its capture into the step graph. With two or
+more GPUs visible, two processes on two GPUs run the RCCL transport for real (rank-ordered
+ncclAllGather of the reduced camera system, all-reduces of the iteration/decision terms)."""
 import numpy as np
 import pytest
 
@@ -99,6 +100,35 @@ def test_four_ranks_host_transport_match_oracle(tmp_path, cfg):
     for x in r:
         assert int(x["local_landmarks"]) == int(x["plan_landmarks"]) and int(x["local_edges"]) == int(x["plan_edges"])
     _check(r[0], oa.lba_plucker(g))
+
+
+def _visible_gpus() -> int:
+    import torch
+    return torch.cuda.device_count()  # (does not initialise the GPU on this image)
+
+
+@pytest.mark.skipif(_visible_gpus() < 2, reason="needs two GPUs (one RCCL rank per GPU)")
+@pytest.mark.parametrize("cfg", ["C2", "C5"])
+def test_two_ranks_rccl_two_gpus_match_oracle(tmp_path, cfg):
+    """One process per GPU over the library's RCCL communicator: the rank-ordered all-gather
+    exchange (k_rcs_blockpart -> ncclAllGather -> k_rcs_xunpack) that the host transport only
+    emulates by a zero-padded sum. Every rank must return the identical result, equal to the oracle
+    and bitwise equal to the same window over the host transport."""
+    import torch.multiprocessing as mp
+    world = 2
+    res = {}
+    for transport in ("rccl", "host"):
+        d = tmp_path / transport
+        d.mkdir()
+        mp.spawn(dw.sharded_gpu_worker, args=(world, dw.free_port(), str(d), cfg, transport, False,
+                                              transport == "rccl"), nprocs=world, join=True)
+        res[transport] = [dict(np.load(d / f"rank{i}.npz")) for i in range(world)]
+    r = res["rccl"]
+    for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2", "ept_level", "iters", "trace_chi2"):
+        assert np.array_equal(r[0][k], r[1][k]), k
+        assert np.array_equal(r[0][k], res["host"][0][k]), ("rccl vs host", k)
+    assert all(bool(x["rerun_equal"]) for x in r)
+    _check(r[0], oa.lba_plucker(synth.generate(cfg)))
 
 
 def test_one_rank_rccl_transport_matches_oracle():

@@ -89,6 +89,114 @@ __global__ __launch_bounds__(64 * NW) void k_ll(double *out, unsigned long long 
     if (tid == 0) cyc[0] = t1 - t0;
 }
 
+// two independent chains in one wave (the two segments of the two-sided elimination): how much of
+// one chain's latency does the other chain's work fill?
+__global__ __launch_bounds__(64) void k_ll2(double *out, unsigned long long *cyc, int reps) {
+    __shared__ __attribute__((aligned(16))) double Sb[2][2][36], Ar[36], An[36];
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < 36) {
+        const int r = tid / 6, c = tid % 6;
+        Sb[0][0][tid] = Sb[1][0][tid] = r == c ? 4.0 + 0.1 * r : 0.2 / (1 + r + c);
+        Ar[tid] = (r == c ? 0.5 : 0.05) / (1 + r);
+        An[tid] = r == c ? 4.0 + 0.1 * r : 0.2 / (1 + r + c);
+    }
+    __syncthreads();
+    const int r = lane < 36 ? lane / 6 : 0, c = lane < 36 ? lane % 6 : 0;
+    bool fail = false;
+    unsigned long long t0 = 0, t1 = 0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+    for (int k = 0; k < reps; ++k) {
+        const int par = k & 1;
+        double s[2][21], dinv[2][6], ar[6], ac[6], u[2][6], v[2][6];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = 0; j <= i; ++j) s[h][tri(i, j)] = Sb[h][par][i * 6 + j];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) { ar[m] = Ar[r * 6 + m]; ac[m] = Ar[c * 6 + m]; }
+        const double anrc = An[r * 6 + c];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ldl6(s[h], dinv[h], fail);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) { lsolve6(s[h], ar, u[h]); lsolve6(s[h], ac, v[h]); }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            double acc = 0.0;
+#pragma unroll
+            for (int m = 0; m < 6; ++m) acc = fma(u[h][m] * dinv[h][m], v[h][m], acc);
+            if (lane < 36) Sb[h][par ^ 1][lane] = anrc - acc;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    if (tid < 36) out[tid] = Sb[0][reps & 1][tid] + Sb[1][reps & 1][tid] + (fail ? 1.0 : 0.0);
+    if (tid == 0) cyc[0] = t1 - t0;
+}
+
+__device__ __forceinline__ double rl64(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+// the column-lane step of plba_band_cl.hpp (cross-lane Gauss-Jordan on pivot lanes 0..5, then
+// v <- o - a1·v with a1, o from LDS), H independent chains interleaved in one wave
+template <int H>
+__global__ __launch_bounds__(64) void k_gj(double *out, unsigned long long *cyc, int reps) {
+    __shared__ __attribute__((aligned(16))) double A1[36], O[64 * 6];
+    const int lane = threadIdx.x;
+    if (lane < 36) A1[lane] = (lane / 6 == lane % 6 ? 0.3 : 0.01);
+    for (int r = 0; r < 6; ++r) O[lane * 6 + r] = (lane % 6 == r ? 4.0 : 0.1);
+    __syncthreads();
+    double v[H][6];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+        for (int r = 0; r < 6; ++r) v[h][r] = O[lane * 6 + r] + 0.01 * h;
+    bool fail = false;
+    unsigned long long t0 = 0, t1 = 0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+    for (int k = 0; k < reps; ++k) {
+#pragma unroll
+        for (int p = 0; p < 6; ++p) {
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                double f[6];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) f[r] = rl64(v[h][r], p);
+                fail = fail || f[p] == 0.0;
+                const double rp = rcp_nr1(f[p]);
+                const double mp = v[h][p] * rp;
+#pragma unroll
+                for (int r = 0; r < 6; ++r) v[h][r] = r == p ? mp : fma(-f[r], mp, v[h][r]);
+            }
+        }
+        double a1[36], o[6];
+#pragma unroll
+        for (int q = 0; q < 36; ++q) a1[q] = A1[q];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) o[r] = O[lane * 6 + r];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+            double acc[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int m = 0; m < 6; ++m)
+#pragma unroll
+                for (int r = 0; r < 6; ++r) acc[r] = fma(a1[r * 6 + m], v[h][m], acc[r]);
+#pragma unroll
+            for (int r = 0; r < 6; ++r) v[h][r] = o[r] - acc[r];
+        }
+    }
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    double sum = 0.0;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+        for (int r = 0; r < 6; ++r) sum += v[h][r];
+    out[lane] = sum + (fail ? 1.0 : 0.0);
+    if (lane == 0) cyc[0] = t1 - t0;
+}
+
 // primitive latencies, 64 dependent repetitions each
 template <int V>
 __global__ __launch_bounds__(64) void k_prim(double *out, unsigned long long *cyc, int reps) {
@@ -127,6 +235,15 @@ int main() {
         hipLaunchKernelGGL(k_ll<8>, dim3(1), dim3(512), 0, 0, out, cyc, reps);
         hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
         printf("lane-local step, 8 waves + bar: %.1f cycles/step\n", (double)c / reps);
+        hipLaunchKernelGGL(k_ll2, dim3(1), dim3(64), 0, 0, out, cyc, reps);
+        hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+        printf("two chains in one wave:         %.1f cycles/double step\n", (double)c / reps);
+        hipLaunchKernelGGL(k_gj<1>, dim3(1), dim3(64), 0, 0, out, cyc, reps);
+        hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+        printf("column-lane GJ step, 1 chain:   %.1f cycles/step\n", (double)c / reps);
+        hipLaunchKernelGGL(k_gj<2>, dim3(1), dim3(64), 0, 0, out, cyc, reps);
+        hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+        printf("column-lane GJ step, 2 chains:  %.1f cycles/double step\n", (double)c / reps);
         const char *nm[] = {"dependent fma", "rcp_nr1 + add", "LDS write->read"};
         for (int v = 0; v < 3; ++v) {
             if (v == 0) hipLaunchKernelGGL(k_prim<0>, dim3(1), dim3(64), 0, 0, out, cyc, reps);
