@@ -1267,7 +1267,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         // one staging block: Tcw | pt_xyz | ln_orth | χ² (doubles), then the byte outputs
         ALLOC(ctx->d_outd, out_doubles(n_kf, n_pt, n_ln, E) + ((size_t)Ep + E + 7) / 8);
     }
-#ifdef PLBA_STAMPS
+#if defined(PLBA_STAMPS) || defined(PLBA_PHASE_STAMPS)
     ZALLOC(d.stamps, 17 * 8);
 #endif
 #undef ALLOC
@@ -2203,7 +2203,7 @@ int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *la
 
 // Diagnostic build only: per-wave, per-phase cycle sums of the banded factorisation.
 int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [17][8] */) {
-#ifdef PLBA_STAMPS
+#if defined(PLBA_STAMPS) || defined(PLBA_PHASE_STAMPS)
     if (!ctx || !ctx->d.stamps) return PLBA_E_STATE;
     PLBA_CHECK(d2h(ctx, out, ctx->d.stamps, 17 * 8 * sizeof(unsigned long long)));
     return PLBA_OK;
@@ -2232,7 +2232,7 @@ int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap) {
                            ctx->d.band_mode, ctx->d.nch, ctx->n_free_edges, ctx->d.Ep,
                            ctx->step_exec != nullptr, ctx->d.sharded, ctx->d.twisted, ctx->d.cl, ctx->d.bcr_N,
                            ctx->d.dense_mfma, ctx->bcr_fallbacks, ctx->d.spec_max, ctx->d.spec_policy,
-                           ctx->h_ctrl ? ctx->h_ctrl->steps : 0, 0, ctx->dev_build};  // [20]: unused (was the four-segment flag)
+                           ctx->h_ctrl ? ctx->h_ctrl->steps : 0, 0, ctx->dev_build};  // [20]: unused
     for (int i = 0; i < cap && i < 22; ++i) out[i] = v[i];
     return PLBA_OK;
 }

@@ -5,11 +5,13 @@
 //
 // * The critical wave holds the whole current block column k of the band in registers, one
 //   lane per scalar column of block row k: lane 6s+c carries column c of A_{k,i} (the block of
-//   row i ≡ s mod W), lane 6W carries the right-hand side y_k. Eliminating block k is then a
-//   6-pivot Gauss–Jordan *across lanes* in which every lane transforms its own 6-vector: the
-//   pivot column is broadcast with v_readlane (SGPR operands, no LDS round trip), the pivot is
-//   inverted with v_rcp_f64 + 2 Newton steps. The result is X_i = S_k⁻¹A_{k,i} = L_{i,k}ᵀ for
+//   row i ≡ s mod W), lane 6W carries the right-hand side y_k. Eliminating block k: the column
+//   is published to LDS (the workers need it anyway), every lane reads the pivot block S_k back,
+//   factors it LDLᵀ in its own registers (no cross-lane dependency; v_rcp_f64 + one Newton step
+//   per pivot) and solves its own 6-vector. The result is X_i = S_k⁻¹A_{k,i} = L_{i,k}ᵀ for
 //   every band block at once, and z_k = S_k⁻¹y_k — no separate S⁻¹ and no separate L product.
+//   (Rounds 2-4 broadcast the pivot column of a cross-lane Gauss–Jordan with v_readlane: 72 per
+//   step, the largest single cost of the step.)
 // * The next column k+1 (the next pivot's block column) is formed by the same wave right after
 //   the single workgroup barrier: A_{i,k+1} -= L_{i,k}A_{k+1,k}ᵀ with A_{k+1,k} read from LDS
 //   while the X publish and the barrier run.
@@ -21,7 +23,8 @@
 //
 // Reference semantics: src/mapHandler.cpp:5925-5927 solves with LinearSolverEigen =
 // SimplicialLDLT: no pivoting, failure iff a pivot is zero. The pivots of the
-// 6x6 Gauss–Jordan are exactly the LDLᵀ pivots, so a zero one fails the solve the same way.
+// lane-local 6x6 LDLᵀ of each pivot block are exactly LDLᵀ pivots of the system, so a zero one
+// fails the solve the same way.
 
 constexpr int kClNT = 512;     // 1 critical wave + 7 worker waves (2 waves per SIMD)
 constexpr int kClMaxBW = 9;    // 6(bw+1) column lanes + 1 rhs lane must fit one wave
@@ -93,11 +96,13 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
     constexpr int NRHS = (BW - 1) * 6;              // right-hand-side tasks
     constexpr int NROW = W * 36 + 6;                // block row streamed in per step
     constexpr int NFL = BW * 36 + 6;                // L blocks + z flushed per step
-    static_assert(NPT6 + NRHS <= NW && NROW <= NW && NFL <= NW, "one task of each kind per worker");
+    constexpr int NWX = NW;
+    static_assert(NPT6 + NRHS <= NWX && NROW <= NWX && NFL <= NWX, "one task of each kind per worker");
     static_assert(6 * W + 1 <= 64, "column lanes + rhs lane must fit one wave");
     const int nrows = g.nrows;
     double *win = lds, *bwin = win + W1 * W * 36, *preA = bwin + W1 * 6, *Xs = preA + 2 * W * 36;
-    const int tid = threadIdx.x, lane = tid & 63, wt = tid - 64;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wt = tid - 64;
     const bool crit = tid < 64;
     if (load_window) {
         for (int t = tid; t < W1 * W * 36; t += NT) {
@@ -140,7 +145,7 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
         r_wi = 2 + (wt - NPT6) / 6;
         r_a = (wt - NPT6) % 6;
     }
-    const int fl = NW - 1 - wt;                     // flush task (counted from the last worker)
+    const int fl = NWX - 1 - wt;                    // flush task (counted from the last worker)
     // ---- worker prefetch ring: block row k+2+bw for step k
     double wpf[PD];
     auto prefetch = [&](int k, double &wdst) {
@@ -174,9 +179,11 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
                 }
                 double a1[36];
                 STAMP(0);
-#ifdef PLBA_CL_LL
-                // B': every lane factors S_k = A_{k,k} (the pivot group's published columns) in its
-                // own registers and applies S_k⁻¹ to its own column: no cross-lane dependency
+                // B: every lane factors S_k = A_{k,k} (the pivot group's just-published columns) in
+                // its own registers and applies S_k⁻¹ to its own column (X_i = L_{i,k}ᵀ, z_k on the
+                // rhs lane). Replaces a Gauss–Jordan across the lanes whose 72 v_readlane a step were
+                // ~35 % of the step (tools/micro/cl_step.hip): the real kernel's forward step
+                // 2,360 -> 2,200 cycles (phase stamps, C3).
                 {
                     double s[21], dv[6];
                     const double *Sk = pA + sk * 36;  // entry (r, c) at [c * 6 + r]
@@ -189,21 +196,6 @@ __device__ __forceinline__ void cl_forward(const BandSeg &g, int k0, int k1, boo
                     if (zp) fail = true;
                     ldl6_solve(s, dv, v);
                 }
-#else
-                // B: Gauss–Jordan on block row k across the lanes (pivot lanes 6*sk + p)
-#pragma unroll
-                for (int p = 0; p < 6; ++p) {
-                    const int pl = 6 * sk + p;
-                    double f[6];
-#pragma unroll
-                    for (int r = 0; r < 6; ++r) f[r] = readlane_f64(v[r], pl);
-                    if (f[p] == 0.0) fail = true;
-                    const double rp = rcp_nr1(f[p]);
-                    const double mp = v[p] * rp;
-#pragma unroll
-                    for (int r = 0; r < 6; ++r) v[r] = r == p ? mp : fma(-f[r], mp, v[r]);
-                }
-#endif
                 // A_{k+1,k} only feeds E/F: read after the Gauss–Jordan, so B does not wait for
                 // 18 broadcast reads (C and the barrier cover their latency; the sched_barrier
                 // keeps the scheduler from sinking them to their use): step 2,696 -> 2,570 cycles
@@ -388,7 +380,7 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d0) {
         const size_t sep_stride = (size_t)BW * W * 36 + (size_t)BW * 6;
         double *sep0 = d.tw_sep, *sep1 = d.tw_sep + sep_stride;
         bool fail = false;
-#ifdef PLBA_STAMPS
+#if defined(PLBA_STAMPS) || defined(PLBA_PHASE_STAMPS)  // (phase marks alone: no per-step stamps)
         unsigned long long t0 = __builtin_readcyclecounter();
 #define CL_MARK(q)                                                                       \
     do {                                                                                 \

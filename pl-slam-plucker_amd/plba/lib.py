@@ -293,7 +293,7 @@ class Solver:
                     chunks=st[7], free_edges=st[8], point_edges=st[9], graph=st[10], sharded=st[11],
                     twisted=st[12], column_lane=st[13], bcr_rows=st[14], dense_mfma=st[15],
                     bcr_fallbacks=st[16], spec_slots=st[17], spec_policy=st[18], device_steps=st[19],
-                    factor_kind=st[20], device_build=st[21])
+                    unused20=st[20], device_build=st[21])
 
     def synchronize(self):
         self._check(self.L.plba_synchronize(self.ctx), "plba_synchronize")
