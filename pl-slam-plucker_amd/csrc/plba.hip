@@ -425,14 +425,24 @@ inline bool want_bcr(int bw, int nf, int resident) {
 struct SpecChoice {
     int slots, policy;
 };
-inline SpecChoice spec_choice(bool cl, bool sharded, bool has_trials, int64_t E) {
+// bcr_fit: how many BCR factorisations the device holds at once (resident workgroups / super-rows);
+// trial slots of a BCR window run side by side only if they all fit (else the second slot's
+// super-rows would wait for the first's to retire and the levels would serialise). A/B at C4
+// (DESIGN §2): 1,551 -> 1,817 LM it/s (31 -> 22 steps per LBA); PLBA_SPEC_BCR=0 disables.
+inline SpecChoice spec_choice(bool cl, bool bcr, int bcr_fit, bool sharded, bool has_trials) {
     SpecChoice r{1, kSpecOff};
-    if (!cl || sharded || !has_trials) return r;
-    (void)E;
+    if (sharded || !has_trials || !(cl || bcr)) return r;
+    int cap = kMaxSpec;
+    if (bcr) {
+        const char *b = getenv("PLBA_SPEC_BCR");
+        if ((b && b[0] == '0') || bcr_fit < 2) return r;
+        cap = std::min(cap, bcr_fit);
+    }
     r.slots = 2;
     r.policy = kSpecSticky;
     const char *e = getenv("PLBA_SPEC");
     if (e && e[0]) r.slots = std::max(1, std::min(atoi(e), kMaxSpec));
+    r.slots = std::min(r.slots, cap);
     const char *p = getenv("PLBA_SPEC_POLICY");
     if (p && p[0]) r.policy = std::max(0, std::min(atoi(p), 3));
     if (r.policy == kSpecOff) r.slots = 1;
@@ -443,9 +453,10 @@ inline SpecChoice spec_choice(bool cl, bool sharded, bool has_trials, int64_t E)
 inline hipError_t launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
     if (d.bcr) {  // forward elimination, then back substitution + pose update (plba_bcr.hpp)
-        hipError_t e = hipLaunchKernel(bcr_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrNT), args, bcr_lds_bytes(d.bw), s);
+        hipError_t e = hipLaunchKernel(bcr_kernel(d.bw), dim3(d.bcr_N, d.spec_max), dim3(kBcrNT), args, bcr_lds_bytes(d.bw), s);
         if (e != hipSuccess) return e;
-        return hipLaunchKernel(bcr_back_kernel(d.bw), dim3(d.bcr_N), dim3(kBcrBackNT), args, bcr_back_lds_bytes(d.bw), s);
+        return hipLaunchKernel(bcr_back_kernel(d.bw), dim3(d.bcr_N, d.spec_max), dim3(kBcrBackNT), args,
+                               bcr_back_lds_bytes(d.bw), s);
     }
     if (d.cl) {
         const void *k = cl_kernel_impl(d.bw, d.twisted != 0, std::make_integer_sequence<int, kClMaxBW + 1>{});
@@ -1015,7 +1026,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // two-sided factorisation when the chain is long enough to halve and the separator's dense
     // system fits next to the band window in LDS (PLBA_NO_TWIST=1 disables, diagnostics only)
     const char *no_twist = getenv("PLBA_NO_TWIST");
-    const bool bcr = band_mode && !ctx->no_bcr && want_bcr(bw, nf, bcr_resident(ctx->opts.device, bw));
+    const int bcr_res = band_mode && !ctx->no_bcr ? bcr_resident(ctx->opts.device, bw) : 0;
+    const bool bcr = band_mode && !ctx->no_bcr && want_bcr(bw, nf, bcr_res);
     d.bcr = bcr ? 1 : 0;
     d.bcr_N = bcr ? (nf + bw - 1) / bw : 0;
     const bool cl = band_mode && !bcr && use_cl(bw);
@@ -1037,10 +1049,12 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.corrected = ctx->opts.corrected_line_jacobian;
     // Speculative trials: worth it where the step is bound by the serial factorisation
     // chain and the rest of the chip idles during it — the column-lane factorisation (one or two
-    // workgroups per trial); the extra slots' edge and landmark kernels are then the price.
-    // Not for BCR (every CU already busy), the dense path or sharded windows (collectives per slot).
+    // workgroups per trial) and BCR windows whose slots' super-rows all fit the device at once;
+    // the extra slots' edge and landmark kernels are then the price. Not for the dense path or
+    // sharded windows (collectives per slot).
     {
-        const SpecChoice sp = spec_choice(d.cl != 0, sharded, n_lm > 0 && nch > 0, E);
+        const SpecChoice sp = spec_choice(d.cl != 0, bcr, bcr ? bcr_res / std::max(d.bcr_N, 1) : 0, sharded,
+                                          n_lm > 0 && nch > 0);
         d.spec_max = sp.slots;
         d.spec_policy = sp.policy;
         d.nbs = d.spec_max + 1;
@@ -1197,14 +1211,22 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         ZALLOC(d.tw_fail, 2 * (size_t)W);
         ZALLOC(d.tw_count, (size_t)W);
     }
-    if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate
-        ALLOC(d.bcr_pub, (size_t)d.bcr_N * bcr_pub_doubles(bw));
-        ALLOC(d.bcr_x, (size_t)d.bcr_N * bcr_xrec(bw));
-        ALLOC(d.bcr_X, (size_t)d.bcr_N * bcr_X_doubles(bw));
+    if (bcr) {  // flags carry epochs from bcr_ctl[0]: start from a clean slate (one set per trial slot)
+        const int64_t N = d.bcr_N;
+        d.bcr_sl[0] = N * (int64_t)bcr_pub_doubles(bw);
+        d.bcr_sl[1] = N * (int64_t)bcr_xrec(bw);
+        d.bcr_sl[2] = N * (int64_t)bcr_X_doubles(bw);
+        d.bcr_sl[3] = 2 * N;
+        d.bcr_sl[4] = kBcrCtl;
+        d.bcr_sl[5] = N * (int64_t)kBcrStamps;
+        ALLOC(d.bcr_pub, (size_t)W * d.bcr_sl[0]);
+        ALLOC(d.bcr_x, (size_t)W * d.bcr_sl[1]);
+        ALLOC(d.bcr_X, (size_t)W * d.bcr_sl[2]);
+
         UPLOAD(d.h_kf, h_kf);
-        ZALLOC(d.bcr_flag, 2 * (size_t)d.bcr_N);
-        ZALLOC(d.bcr_ctl, kBcrCtl);
-        ZALLOC(d.bcr_stamps, (size_t)d.bcr_N * kBcrStamps);
+        ZALLOC(d.bcr_flag, (size_t)W * d.bcr_sl[3]);
+        ZALLOC(d.bcr_ctl, (size_t)W * kBcrCtl);
+        ZALLOC(d.bcr_stamps, (size_t)W * d.bcr_sl[5]);
         // the schedule's starting state, restored if a hand-off wait times out (run_schedule)
         ctx->alloc(ctx->bk_T, (size_t)n_kf * 12);
         ctx->alloc(ctx->bk_X, (size_t)std::max(n_lm, 1) * 4);

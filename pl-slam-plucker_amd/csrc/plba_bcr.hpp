@@ -224,8 +224,8 @@ constexpr int kBcrStamps = 32;
 __device__ __forceinline__ int gtile(int u, int v) { return u * (u + 1) / 2 + v; }
 
 template <int BW>
-__global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)  // trial slot s: its own band, records, flags and tickets (slot_view)
     if constexpr (BW >= 1 && BW <= kBcrMaxBW) {
         constexpr int NT = kBcrNT, S = 6 * BW, NB = 2 * BW + 1, RS = 6 * NB, WS = S + RS;
         constexpr int TRI = bcr_tri(BW), NRT = BW * NB, NG = bcr_ngram(BW), NX = 2 * S + 1;
@@ -573,7 +573,8 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
             for (int t = tid; t < S * NX; t += NT) Xg[t] = Rm[(t / NX) * RS + t % NX];
         } else {
             for (int r = tid; r < S; r += NT) st_sc1(d.bcr_x + r, Rm[r * RS + 2 * S]);
-            if (tid == 0) d.ctrl->solve_ok[0] = fail_fwd != 0.0 ? 0 : 1;  // every failure word has flowed in
+            // every failure word has flowed in (PLBA_DIAG bit 128: the tests' forced failures)
+            if (tid == 0) *d.solve_okp = (fail_fwd != 0.0 || diag_fail(d)) ? 0 : 1;
             bcr_publish(&d.bcr_flag[1], epoch);
         }
         BCR_STAMP(16);
@@ -595,8 +596,8 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d) {
 // trial state, x_p kept from the previous trial when the solve failed — A13 — and the pose part of
 // Σx(λx+b) per row; fixed poses k ≡ m (mod N) copied to the trial state).
 template <int BW>
-__global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d) {
-    TRIAL_GUARD
+__global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d0) {
+    TRIAL_SLOT(blockIdx.y)
     if constexpr (BW >= 1 && BW <= kBcrMaxBW) {
         constexpr int NT = kBcrBackNT, S = 6 * BW, NX = 2 * S + 1, XR = bcr_xrec(BW);
         constexpr int NPART = NT / S < kBcrParts ? NT / S : kBcrParts;  // mat-vec slices per row
@@ -627,20 +628,19 @@ __global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d) {
             const double *Xg = d.bcr_X + (size_t)m * S * NX;
             for (int t = tid; t < S * NX; t += NT) Xm[t] = Xg[t];
         }
-        const int cur0 = d.ctrl->cur;
-        const double *Tc0 = d.Tb[cur0];
-        double *Tt0 = d.Tb[cur0 ^ 1];
+        const double *Tc0 = d.Tc;  // (slot view: this slot's trial buffer)
+        double *Tt0 = d.Tt;
         if (tid < BW) s_kf[tid] = m * BW + tid < nf ? d.h_kf[m * BW + tid] : 0;
         for (int t = tid; t < BW * 24; t += NT) {
             const int i = t / 24, q = t % 24, h = m * BW + i;
             double v = 0.0;
             if (h < nf) {
                 const int kf = d.h_kf[h];
-                v = q < 12 ? Tc0[(size_t)kf * 12 + q] : (q < 18 ? d.bp[(size_t)h * 6 + q - 12] : d.xp[(size_t)h * 6 + q - 18]);
+                v = q < 12 ? Tc0[(size_t)kf * 12 + q] : (q < 18 ? d.bp[(size_t)h * 6 + q - 12] : d.xp_prev[(size_t)h * 6 + q - 18]);
             }
             ps[t] = v;
         }
-        if (tid == 0) ps[BW * 24] = d.ctrl->lambda;
+        if (tid == 0) ps[BW * 24] = d.lam;
         const bool hlm0 = d.ctrl->hlm != 0;
         for (int k = m + N * tid; k < d.n_kf; k += N * NT)
             if (d.kf_hidx[k] < 0) {
@@ -648,7 +648,7 @@ __global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d) {
                 for (int q = 0; q < 12; ++q) Tt0[(size_t)k * 12 + q] = Tc0[(size_t)k * 12 + q];
                 if (hlm0)
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) d.xk[cur0 ^ 1][(size_t)k * 6 + q] = d.xk[cur0][(size_t)k * 6 + q];
+                    for (int q = 0; q < 6; ++q) d.xkt[(size_t)k * 6 + q] = d.xkc[(size_t)k * 6 + q];
             }
         if (!root) {
             // (a timeout raises Ctrl::dev_error: the host discards this schedule and re-solves)
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d) {
         }
         // ---- this super-row's poses: x_p (kept from the previous trial if the solve failed, A13),
         //      oplus into the trial state, pose part of Σx(λx+b)
-        const bool failed = d.ctrl->solve_ok[0] == 0;
+        const bool failed = *d.solve_okp == 0;
         const double lam = ps[BW * 24];
         double sc = 0.0;
         if (tid < BW) {
@@ -705,13 +705,13 @@ __global__ __launch_bounds__(kBcrBackNT) void k_rcs_bcr_back(Dev d) {
                     double xn[6];
 #pragma unroll
                     for (int q = 0; q < 6; ++q) sc += x[q] * x[q];
-                    hlm_pose_update(d.xk[cur0] + (size_t)kf * 6, x, xn, d.Tb[cur0 ^ 1] + (size_t)kf * 12);
+                    hlm_pose_update(d.xkc + (size_t)kf * 6, x, xn, Tt0 + (size_t)kf * 12);
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) d.xk[cur0 ^ 1][(size_t)kf * 6 + q] = xn[q];
+                    for (int q = 0; q < 6; ++q) d.xkt[(size_t)kf * 6 + q] = xn[q];
                 } else {
 #pragma unroll
                     for (int q = 0; q < 6; ++q) sc += x[q] * (lam * x[q] + pp[12 + q]);
-                    pose_oplus(pp, x, d.Tb[cur0 ^ 1] + (size_t)s_kf[tid] * 12);
+                    pose_oplus(pp, x, Tt0 + (size_t)s_kf[tid] * 12);
                 }
             }
         }

@@ -209,6 +209,7 @@ struct Dev {
     uint32_t *bcr_flag;                 // [N][2] forward / backward hand-off flags (epoch)
     uint32_t *bcr_ctl;                  // [kBcrCtl] epoch, forward arrivals / tickets, backward arrivals / tickets
     unsigned long long *bcr_stamps;     // [N][32] phase timestamps (PLBA_DIAG bit 8 only)
+    int64_t bcr_sl[6];                  // per trial slot strides of bcr_pub, _x, _X, _flag, _ctl, _stamps
 };
 
 
@@ -274,6 +275,14 @@ __device__ __forceinline__ Dev slot_view(const Dev &d0, int s) {
             d.tw_sep += ss * sl_sep(d0);
             d.tw_fail += 2 * ss;
             d.tw_count += ss;
+        }
+        if (d0.bcr) {
+            d.bcr_pub += ss * d0.bcr_sl[0];
+            d.bcr_x += ss * d0.bcr_sl[1];
+            d.bcr_X += ss * d0.bcr_sl[2];
+            d.bcr_flag += ss * d0.bcr_sl[3];
+            d.bcr_ctl += ss * d0.bcr_sl[4];
+            d.bcr_stamps += ss * d0.bcr_sl[5];
         }
         d.part_lm += ss * sl_lms(d0);
         d.part_lms += ss * sl_lms(d0);

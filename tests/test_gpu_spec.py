@@ -118,6 +118,26 @@ def test_speculative_slot_width_changes_on_an_oversubscribed_grid():
             _assert_same(base, out2, (slots, pol, "second schedule"))
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+def test_speculative_slots_on_block_cyclic_reduction_are_bitwise(cfg):
+    """Trial slots on BCR windows (on by default when the slots' super-rows fit the device): each
+    slot runs its own ticketed BCR launch
+    (records, flags, tickets and epochs per slot, grid.y = slot). Bitwise the one-slot solve, with
+    forced solve failures too (C2: BCR forced on a short window; C4: its natural choice)."""
+    with _Env(PLBA_FACTOR="bcr", PLBA_SPEC_BCR=1):
+        g = synth.generate(cfg)
+        for diag in (0, 128):
+            base, base2, st0 = _solve(g, 1, 0, diag=diag)
+            assert st0["bcr_rows"] > 0 and st0["spec_slots"] == 1, st0
+            _assert_same(base, base2, "rerun")
+            for slots, pol in ((2, 1), (2, 3), (3, 2)):
+                out, out2, st = _solve(g, slots, pol, diag=diag)
+                assert st["bcr_rows"] > 0 and st["spec_slots"] == slots, st
+                _assert_same(base, out, (slots, pol, diag))
+                _assert_same(base, out2, (slots, pol, diag, "second schedule"))
+                assert st["device_steps"] <= st0["device_steps"], (st, st0)
+
+
 def test_speculative_zero_pivot_window():
     """τ = 0 and a keyframe with zero information: every solve fails (λ stays 0), every slot's
     trial is rejected with the previous x and optimize(5) terminates after maxTrials."""
