@@ -312,6 +312,7 @@ def main():
         a.config = "C5"
     base_seed = synth.CONFIGS[a.config][3]
     dev = local if a.device is None else a.device
+    create_ms = None
     if shard:  # one window for all ranks
         g = synth.generate(a.config, seed=base_seed)
         if dist is None:
@@ -326,7 +327,9 @@ def main():
             s = sharded_solver(device=dev, transport=a.transport)
     else:
         g = synth.generate(a.config, seed=base_seed + 97 * rank)
+        t0 = time.perf_counter()
         s = Solver(device=dev)
+        create_ms = (time.perf_counter() - t0) * 1e3
     t0 = time.perf_counter()
     s.upload(g)
     s.synchronize()
@@ -511,6 +514,9 @@ def main():
                 "lm_iterations_per_lba": it_per_lba,
                 "trials_per_lba": trials / a.steps,
                 "ms_per_lm_iteration": dt / max(iters, 1) * 1e3,
+                # plba_create pre-warms the context (code objects, first device build, pinned
+                # staging): create_ms is that one-time cost, upload_ms the process's first window
+                "create_ms": create_ms,
                 "upload_ms": upload_ms,
                 "end_to_end": e2e[-1],
                 "factorisation": ("block cyclic reduction over %d super-rows" % info["bcr_rows"] if info.get("bcr_rows")

@@ -1427,7 +1427,7 @@ int launch_step(plba_ctx *ctx) {
     Dev &d = ctx->d;
     hipStream_t s = ctx->stream;
     // PLBA_CHUNK_DIRECT=1: per-lane A/Z row loads in the Schur assembly (A/B of the staged copy)
-    static const bool chunk_direct = getenv("PLBA_CHUNK_DIRECT") != nullptr;
+    const bool chunk_direct = getenv("PLBA_CHUNK_DIRECT") != nullptr;  // (read per capture: tests switch it)
 
     if (d.E > 0) LAUNCH(K_LINEARIZE, hipLaunchKernelGGL(k_linearize, dim3(d.n_lin_blocks), dim3(kBlock), 0, s, d));
     if (d.nf > 0 || d.n_lm > 0) {
@@ -1546,12 +1546,9 @@ int capture_steps(plba_ctx *ctx, int nsteps, hipGraph_t &graph, hipGraphExec_t &
 // updated in place only for a window with the same signature (hipGraphExecUpdate changes kernel
 // arguments and grids, never the kernel a node runs).
 // multi-step graphs captured: 2, 4, .. 2^L steps (PLBA_GRAPH_LEVELS overrides, for measurements)
-int graph_levels() {
-    static const int L = [] {
-        const char *e = getenv("PLBA_GRAPH_LEVELS");
-        return e ? std::max(0, std::min(atoi(e), (int)plba_ctx::kMultiLevels)) : (int)plba_ctx::kMultiLevels;
-    }();
-    return L;
+int graph_levels() {  // (read per capture: tests switch it)
+    const char *e = getenv("PLBA_GRAPH_LEVELS");
+    return e ? std::max(0, std::min(atoi(e), (int)plba_ctx::kMultiLevels)) : (int)plba_ctx::kMultiLevels;
 }
 std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
     const Dev &d = ctx->d;
@@ -1875,6 +1872,55 @@ void plba_default_opts(plba_opts *o) {
     o->tau = 1e-5;
 }
 
+// A three-keyframe window with points and a line solved once through the whole path (device
+// build, step graphs, every kernel of a step, output scatter); the context is left without a
+// window, as plba_create returns it.
+int prewarm(plba_ctx *ctx) {
+    constexpr int nk = 3, np = 4, nl = 1, nep = 8, nel = 2;
+    double T[nk * 12] = {0};
+    for (int k = 0; k < nk; ++k) {
+        T[k * 12 + 0] = T[k * 12 + 5] = T[k * 12 + 10] = 1.0;
+        T[k * 12 + 3] = -0.1 * k;  // t_x
+    }
+    const uint8_t fixed[nk] = {1, 0, 0};
+    const int32_t kf_id[nk] = {0, 1, 2}, pt_id[np] = {3, 4, 5, 6}, ln_id[nl] = {8};
+    const double P[np * 3] = {0.3, 0.2, 5.0, -0.4, 0.1, 6.0, 0.1, -0.3, 4.0, -0.2, -0.2, 7.0};
+    const double L[nl * 4] = {0.3, -0.2, 0.4, 0.5};
+    int32_t elm[nep], ekf[nep];
+    double eobs[nep * 2], einfo[nep];
+    const double fx = 458.654, fy = 457.296, cx = 367.215, cy = 248.375;
+    for (int e = 0; e < nep; ++e) {
+        const int l = e % np, k = e / np + (l % 2);  // every point seen twice, all three poses used
+        elm[e] = l;
+        ekf[e] = k;
+        const double x = P[l * 3] + T[k * 12 + 3], y = P[l * 3 + 1], z = P[l * 3 + 2];
+        eobs[e * 2] = fx * x / z + cx + 0.3;
+        eobs[e * 2 + 1] = fy * y / z + cy - 0.2;
+        einfo[e] = 1.0;
+    }
+    const int32_t llm[nel] = {0, 0}, lkf[nel] = {1, 2};
+    const double lobs[nel * 4] = {300, 200, 420, 260, 310, 205, 430, 262}, linfo[nel] = {1.0, 1.0};
+    plba_graph g{};
+    g.n_kf = nk; g.n_pt = np; g.n_ln = nl; g.n_ept = nep; g.n_eln = nel;
+    g.fx = fx; g.fy = fy; g.cx = cx; g.cy = cy;
+    g.kf_Tcw = T; g.kf_fixed = fixed; g.kf_id = kf_id;
+    g.pt_xyz = P; g.pt_id = pt_id; g.ln_orth = L; g.ln_id = ln_id;
+    g.ept_lm = elm; g.ept_kf = ekf; g.ept_obs = eobs; g.ept_info = einfo;
+    g.eln_lm = llm; g.eln_kf = lkf; g.eln_obs = lobs; g.eln_info = linfo;
+    g.huber_pt = g.huber_ln = (double)(float)2.4476519360399;
+    int rc = plba_upload(ctx, &g);
+    if (rc) return rc;
+    double Tout[nk * 12];
+    plba_result res{};
+    res.kf_Tcw = Tout;
+    rc = plba_lba_plucker(ctx, &res);
+    ctx->uploaded = false;  // no window: calls before the caller's own upload stay PLBA_E_STATE
+    ctx->initialized = false;
+    ctx->no_bcr = false;    // (a diagnostic forcing BCR timeouts must not carry over to real windows)
+    ctx->bcr_fallbacks = 0;
+    return rc;
+}
+
 int plba_create(plba_ctx **out, const plba_opts *opts) {
     if (!out) return PLBA_E_INVALID;
     *out = nullptr;
@@ -1896,6 +1942,18 @@ int plba_create(plba_ctx **out, const plba_opts *opts) {
     }
     std::memset(ctx->h_ctrl, 0, sizeof(Ctrl));
     *out = ctx;
+    // Pre-warm (PLBA_NO_PREWARM=1 skips it): the first window of a process otherwise pays the
+    // code-object load, the first rocPRIM sorts of the device window build and the first pinned
+    // staging (C3: first upload 38 ms against 1.2 ms warm) on the LBA thread's first keyframe.
+    const char *npw = getenv("PLBA_NO_PREWARM");
+    if (!(npw && npw[0] == '1')) {
+        const int rc = prewarm(ctx);
+        if (rc) {
+            plba_destroy(ctx);
+            *out = nullptr;
+            return rc;
+        }
+    }
     return PLBA_OK;
 }
 

@@ -153,6 +153,44 @@ def test_column_lane_factorisation_bandwidths(solver, monkeypatch, tmax, n_kf):
     assert np.abs(cl["kf_Tcw"] - old["kf_Tcw"]).max() < 1e-9
 
 
+# Every environment switch the library reads (DESIGN §6 "Switches"), on a window the oracle
+# finishes in seconds: the A/B and diagnostic switches must keep the oracle parity, and those that
+# only change scheduling, load paths, staging or logging must be bitwise the default solve.
+ENV_SWITCHES = [
+    ({"PLBA_NO_FOLD_INIT": "1"}, False),       # k_iter_init as its own launch
+    ({"PLBA_CHUNK_DIRECT": "1"}, True),        # Schur assembly with per-lane row loads
+    ({"PLBA_CHUNK_HALF_MIN": "0"}, False),     # two-lane Schur assembly at any size
+    ({"PLBA_CHUNK_TRIPLES": "64"}, False),     # shorter assembly chunks
+    ({"PLBA_GRAPH_LEVELS": "1"}, True),        # step graphs of 1-2 steps only
+    ({"PLBA_POISON": "1"}, True),              # unwritten arrays start as NaN
+    ({"PLBA_TIMING": "1"}, True),              # host-side phase log
+    ({"PLBA_HOST_BUILD": "1"}, True),          # host window build
+    ({"PLBA_FORCE_DENSE": "1"}, False),        # dense MFMA factorisation of a banded window
+    ({"PLBA_DENSE_SCALAR": "1", "PLBA_FORCE_DENSE": "1"}, False),
+    ({"PLBA_FACTOR": "bcr", "PLBA_SPEC_BCR": "0"}, False),
+    ({"PLBA_FACTOR": "band"}, False),           # 16-wave band kernel
+    ({"PLBA_NO_TWIST": "1"}, False),
+    ({"PLBA_SPEC": "1"}, True),                # one trial slot
+]
+
+
+@pytest.mark.parametrize("env,bitwise", ENV_SWITCHES, ids=lambda x: ",".join(x) if isinstance(x, dict) else str(x))
+def test_environment_switches_keep_parity(solver, monkeypatch, env, bitwise):
+    g = synth.generate("C2")
+    solver.upload(g)
+    base = solver.lba_plucker()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    solver.upload(g)
+    out = solver.lba_plucker()
+    for k in env:
+        monkeypatch.delenv(k)
+    if bitwise:
+        for k in ("kf_Tcw", "pt_xyz", "ln_orth", "ept_chi2", "eln_chi2", "ept_level", "eln_level", "iters", "chi2"):
+            assert np.array_equal(np.asarray(out[k]), np.asarray(base[k])), (env, k)
+    _check(out, oa.lba_plucker(g))
+
+
 def test_empty_graph(solver):
     g = synth.generate("C1", n_pt=0, n_ln=0)
     out, ref = _run(solver, g)

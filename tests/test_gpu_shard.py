@@ -47,6 +47,20 @@ def test_two_ranks_host_transport_match_oracle(tmp_path, cfg):
     _check(r[0], oa.lba_plucker(g))
 
 
+def test_two_ranks_allreduce_exchange_matches_oracle(tmp_path, monkeypatch):
+    """PLBA_SHARD_XCHG=allreduce: the reduced camera system summed by one all-reduce of the whole
+    system (the round-3 exchange) instead of the all-gather of each rank's block-row runs."""
+    import torch.multiprocessing as mp
+    world = 2
+    monkeypatch.setenv("PLBA_SHARD_XCHG", "allreduce")
+    mp.spawn(dw.sharded_gpu_worker, args=(world, dw.free_port(), str(tmp_path), "C2", "host"), nprocs=world,
+             join=True)
+    r = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(world)]
+    for k in ("kf_Tcw", "pt_xyz", "ln_orth", "iters"):
+        assert np.array_equal(r[0][k], r[1][k]), k
+    _check(r[0], oa.lba_plucker(synth.generate("C2")))
+
+
 def test_two_ranks_device_build_equals_host_build(tmp_path):
     """The sharded device window build (k_b_owner + the device sorts) against the host build with
     plba_shard_plan on two ranks: every output bitwise equal."""
