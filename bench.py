@@ -315,16 +315,26 @@ def main():
     create_ms = None
     if shard:  # one window for all ranks
         g = synth.generate(a.config, seed=base_seed)
-        if dist is None:
-            from plba.lib import comm_unique_id
-            s = Solver(device=dev)
-            if a.transport == "rccl":
-                s.comm_init_rccl(1, 0, comm_unique_id())
+        # (RCCL prints a version banner on stdout at communicator init: fd 1 -> stderr meanwhile,
+        # so stdout carries only the JSON line)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if dist is None:
+                from plba.lib import comm_unique_id
+                s = Solver(device=dev)
+                if a.transport == "rccl":
+                    s.comm_init_rccl(1, 0, comm_unique_id())
+                else:
+                    s.comm_init_host(1, 0, lambda buf: None)
             else:
-                s.comm_init_host(1, 0, lambda buf: None)
-        else:
-            from plba.dist import sharded_solver
-            s = sharded_solver(device=dev, transport=a.transport)
+                from plba.dist import sharded_solver
+                s = sharded_solver(device=dev, transport=a.transport)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     else:
         g = synth.generate(a.config, seed=base_seed + 97 * rank)
         t0 = time.perf_counter()

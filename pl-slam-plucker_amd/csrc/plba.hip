@@ -1876,43 +1876,84 @@ void plba_default_opts(plba_opts *o) {
 // build, step graphs, every kernel of a step, output scatter); the context is left without a
 // window, as plba_create returns it.
 int prewarm(plba_ctx *ctx) {
-    constexpr int nk = 3, np = 4, nl = 1, nep = 8, nel = 2;
-    double T[nk * 12] = {0};
+    // Device memory: windows are carved from stream-ordered allocations (hipMallocAsync); keep what
+    // they free in the device's default pool (release threshold: never) and grow the pool once
+    // here (PLBA_PREWARM_MB, default 256 MB of the 288 GB), so that a first window does not pay
+    // the pool's growth; the first pinned upload staging likewise.
+    {
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, ctx->opts.device) == hipSuccess && pool) {
+            uint64_t thr = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+        (void)hipGetLastError();
+        const char *mb = getenv("PLBA_PREWARM_MB");
+        const size_t bytes = (size_t)(mb && mb[0] ? std::max(0, atoi(mb)) : 256) << 20;
+        void *p = nullptr;
+        if (bytes && hipMallocAsync(&p, bytes, ctx->stream) == hipSuccess) (void)hipFreeAsync(p, ctx->stream);
+        (void)hipGetLastError();
+        constexpr size_t kStage = 8u << 20;
+        if (!ctx->staging && hipHostMalloc((void **)&ctx->staging, kStage, hipHostMallocDefault) == hipSuccess)
+            ctx->staging_cap = kStage;
+        (void)hipGetLastError();
+        PLBA_CHECK(hipStreamSynchronize(ctx->stream));
+    }
+    // a window of nk poses, np points and nl lines, each landmark seen by two consecutive poses:
+    // large enough that the device build takes its full-size sort paths (first-call costs of a
+    // small window differ from a real one's)
+    const int nk = 8, np = 4096, nl = 256, nep = 2 * np, nel = 2 * nl;
+    std::vector<double> T((size_t)nk * 12, 0.0), P((size_t)np * 3), L((size_t)nl * 4), eobs((size_t)nep * 2),
+        einfo(nep, 1.0), lobs((size_t)nel * 4), linfo(nel, 1.0);
+    std::vector<uint8_t> fixed(nk, 0);
+    std::vector<int32_t> kf_id(nk), pt_id(np), ln_id(nl), elm(nep), ekf(nep), llm(nel), lkf(nel);
+    fixed[0] = 1;
     for (int k = 0; k < nk; ++k) {
-        T[k * 12 + 0] = T[k * 12 + 5] = T[k * 12 + 10] = 1.0;
-        T[k * 12 + 3] = -0.1 * k;  // t_x
+        T[(size_t)k * 12 + 0] = T[(size_t)k * 12 + 5] = T[(size_t)k * 12 + 10] = 1.0;
+        T[(size_t)k * 12 + 3] = -0.1 * k;  // t_x
+        kf_id[k] = k;
     }
-    const uint8_t fixed[nk] = {1, 0, 0};
-    const int32_t kf_id[nk] = {0, 1, 2}, pt_id[np] = {3, 4, 5, 6}, ln_id[nl] = {8};
-    const double P[np * 3] = {0.3, 0.2, 5.0, -0.4, 0.1, 6.0, 0.1, -0.3, 4.0, -0.2, -0.2, 7.0};
-    const double L[nl * 4] = {0.3, -0.2, 0.4, 0.5};
-    int32_t elm[nep], ekf[nep];
-    double eobs[nep * 2], einfo[nep];
     const double fx = 458.654, fy = 457.296, cx = 367.215, cy = 248.375;
-    for (int e = 0; e < nep; ++e) {
-        const int l = e % np, k = e / np + (l % 2);  // every point seen twice, all three poses used
-        elm[e] = l;
-        ekf[e] = k;
-        const double x = P[l * 3] + T[k * 12 + 3], y = P[l * 3 + 1], z = P[l * 3 + 2];
-        eobs[e * 2] = fx * x / z + cx + 0.3;
-        eobs[e * 2 + 1] = fy * y / z + cy - 0.2;
-        einfo[e] = 1.0;
+    for (int l = 0; l < np; ++l) {
+        pt_id[l] = nk + l;
+        P[(size_t)l * 3] = -1.0 + 2.0 * ((l * 37) % 101) / 101.0;
+        P[(size_t)l * 3 + 1] = -0.8 + 1.6 * ((l * 53) % 97) / 97.0;
+        P[(size_t)l * 3 + 2] = 4.0 + 3.0 * ((l * 29) % 89) / 89.0;
+        for (int o = 0; o < 2; ++o) {
+            const int e = 2 * l + o, k = (l + o) % nk;
+            elm[e] = l;
+            ekf[e] = k;
+            const double x = P[(size_t)l * 3] + T[(size_t)k * 12 + 3], y = P[(size_t)l * 3 + 1], z = P[(size_t)l * 3 + 2];
+            eobs[(size_t)e * 2] = fx * x / z + cx + 0.3;
+            eobs[(size_t)e * 2 + 1] = fy * y / z + cy - 0.2;
+        }
     }
-    const int32_t llm[nel] = {0, 0}, lkf[nel] = {1, 2};
-    const double lobs[nel * 4] = {300, 200, 420, 260, 310, 205, 430, 262}, linfo[nel] = {1.0, 1.0};
+    for (int l = 0; l < nl; ++l) {
+        ln_id[l] = nk + np + 1 + l;
+        L[(size_t)l * 4] = 0.3 + 0.001 * l;
+        L[(size_t)l * 4 + 1] = -0.2;
+        L[(size_t)l * 4 + 2] = 0.4;
+        L[(size_t)l * 4 + 3] = 0.5;
+        for (int o = 0; o < 2; ++o) {
+            const int e = 2 * l + o;
+            llm[e] = l;
+            lkf[e] = (l + o) % nk;
+            const double q[4] = {300.0 + l % 7, 200.0 + o, 420.0, 260.0 + l % 5};
+            for (int c = 0; c < 4; ++c) lobs[(size_t)e * 4 + c] = q[c];
+        }
+    }
     plba_graph g{};
     g.n_kf = nk; g.n_pt = np; g.n_ln = nl; g.n_ept = nep; g.n_eln = nel;
     g.fx = fx; g.fy = fy; g.cx = cx; g.cy = cy;
-    g.kf_Tcw = T; g.kf_fixed = fixed; g.kf_id = kf_id;
-    g.pt_xyz = P; g.pt_id = pt_id; g.ln_orth = L; g.ln_id = ln_id;
-    g.ept_lm = elm; g.ept_kf = ekf; g.ept_obs = eobs; g.ept_info = einfo;
-    g.eln_lm = llm; g.eln_kf = lkf; g.eln_obs = lobs; g.eln_info = linfo;
+    g.kf_Tcw = T.data(); g.kf_fixed = fixed.data(); g.kf_id = kf_id.data();
+    g.pt_xyz = P.data(); g.pt_id = pt_id.data(); g.ln_orth = L.data(); g.ln_id = ln_id.data();
+    g.ept_lm = elm.data(); g.ept_kf = ekf.data(); g.ept_obs = eobs.data(); g.ept_info = einfo.data();
+    g.eln_lm = llm.data(); g.eln_kf = lkf.data(); g.eln_obs = lobs.data(); g.eln_info = linfo.data();
     g.huber_pt = g.huber_ln = (double)(float)2.4476519360399;
     int rc = plba_upload(ctx, &g);
     if (rc) return rc;
-    double Tout[nk * 12];
+    std::vector<double> Tout((size_t)nk * 12);
     plba_result res{};
-    res.kf_Tcw = Tout;
+    res.kf_Tcw = Tout.data();
     rc = plba_lba_plucker(ctx, &res);
     ctx->uploaded = false;  // no window: calls before the caller's own upload stay PLBA_E_STATE
     ctx->initialized = false;

@@ -397,6 +397,16 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d0) {
         cl_forward<BW>(g, 0, mine, true, lds, fail, seg == 0 ? d.stamps : nullptr);
         CL_MARK(seg);
         cl_store_sep<BW>(lds, mine, seg == 0 ? sep0 : sep1);
+        // the separator rows' original band A_sep (the merge subtracts it), loaded while the stores
+        // drain, so the last arriver's merge takes one global round trip instead of two or three
+        constexpr int NWIN = BW * W * 36, NWT = (NWIN + kClNT - 1) / kClNT;
+        double a_sep[NWT], b_sep = 0.0;
+#pragma unroll
+        for (int u = 0; u < NWT; ++u) {
+            const int t = tid + u * kClNT, i = t / (W * 36), rem = t % (W * 36), w = rem / 36;
+            a_sep[u] = t < NWIN && w <= i ? d.Bd[((size_t)(m + i) * W + w) * 36 + rem % 36] : 0.0;
+        }
+        if (tid < BW * 6) b_sep = d.bs[(size_t)(m + tid / 6) * 6 + tid % 6];
         // hand-off: every wave drains its L / z / separator stores, one agent release by lane 0,
         // then the arrival counter; the workgroup whose add returns 1 is last and acquires once
         // before reading the other's data. Exactly two arrivals per launch (both workgroups pass
@@ -420,32 +430,42 @@ __global__ __launch_bounds__(kClNT) void k_rcs_factor_twisted_cl(Dev d0) {
         __syncthreads();
         if (!s_last) return;
         const BandSeg g0{d.Bd, d.bs, d.Lband, nullptr, d.zb, m + BW, m, nullptr};
-        if (seg == 1) {  // segment 0's separator window (rows m..m+bw-1) into this LDS window
-            double *win = lds, *bwin = win + (BW + 2) * W * 36;
-            for (int t = tid; t < (BW + 2) * W * 36; t += kClNT) {
-                const int i = t / (W * 36), rem = t % (W * 36);
-                win[((m + i) % (BW + 2)) * W * 36 + rem] = i < BW ? sep0[t] : 0.0;
-            }
-            for (int t = tid; t < (BW + 2) * 6; t += kClNT) {
-                const int i = t / 6;
-                bwin[((m + i) % (BW + 2)) * 6 + t % 6] = i < BW ? sep0[(size_t)BW * W * 36 + t] : 0.0;
-            }
-        }
-        __syncthreads();
-        // separator rows m+i: + (W1 - A_sep), W1 given in segment 1's reversed numbering
+        // merge: separator rows m+i of the top segment's window += the bottom segment's Schur
+        // contribution (W1: its separator window, reversed numbering, blocks transposed) - A_sep.
+        // As workgroup 1 the last arriver first takes segment 0's window (sep0) from global memory;
+        // both loads go out in one round.
         {
             double *win = lds, *bwin = win + (BW + 2) * W * 36;
             const double *W1 = sep1;
-            for (int t = tid; t < BW * W * 36; t += kClNT) {
-                const int i = t / (W * 36), rem = t % (W * 36), w = rem / 36, e = rem % 36;
-                if (w > i) continue;
+            double w1v[NWT], s0v[NWT];
+#pragma unroll
+            for (int u = 0; u < NWT; ++u) {
+                const int t = tid + u * kClNT, i = t / (W * 36), rem = t % (W * 36), w = rem / 36, e = rem % 36;
+                const bool ok = t < NWIN && w <= i;
                 const int j = i - w, a = e / 6, b = e % 6;
-                win[((m + i) % (BW + 2)) * W * 36 + rem] +=
-                    W1[((size_t)(BW - 1 - j) * W + w) * 36 + b * 6 + a] - d.Bd[((size_t)(m + i) * W + w) * 36 + e];
+                w1v[u] = ok ? W1[((size_t)(BW - 1 - j) * W + w) * 36 + b * 6 + a] : 0.0;
+                s0v[u] = seg == 1 && t < NWIN ? sep0[t] : 0.0;
             }
-            for (int t = tid; t < BW * 6; t += kClNT) {
-                const int i = t / 6, a = t % 6;
-                bwin[((m + i) % (BW + 2)) * 6 + a] += W1[(size_t)BW * W * 36 + (BW - 1 - i) * 6 + a] - d.bs[(size_t)(m + i) * 6 + a];
+            double w1b = 0.0, s0b = 0.0;
+            if (tid < BW * 6) {
+                w1b = W1[(size_t)BW * W * 36 + (BW - 1 - tid / 6) * 6 + tid % 6];
+                s0b = seg == 1 ? sep0[(size_t)BW * W * 36 + tid] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < NWT; ++u) {
+                const int t = tid + u * kClNT, i = t / (W * 36), rem = t % (W * 36), w = rem / 36;
+                if (t >= NWIN) continue;
+                double *dst = win + ((m + i) % (BW + 2)) * W * 36 + rem;
+                const double base = seg == 1 ? s0v[u] : *dst;
+                *dst = w <= i ? base + (w1v[u] - a_sep[u]) : base;
+            }
+            if (tid < BW * 6) {
+                double *dst = bwin + ((m + tid / 6) % (BW + 2)) * 6 + tid % 6;
+                *dst = (seg == 1 ? s0b : *dst) + (w1b - b_sep);
+            }
+            if (seg == 1) {  // window rows m+bw, m+bw+1 (past the separator): zero, as segment 0 left them
+                for (int t = tid; t < 2 * W * 36; t += kClNT) win[((m + BW + t / (W * 36)) % (BW + 2)) * W * 36 + t % (W * 36)] = 0.0;
+                for (int t = tid; t < 2 * 6; t += kClNT) bwin[((m + BW + t / 6) % (BW + 2)) * 6 + t % 6] = 0.0;
             }
         }
         __syncthreads();
