@@ -326,6 +326,7 @@ const void *twisted_kernel_impl(int bw, std::integer_sequence<int, B...>) {
 inline const void *twisted_kernel(int bw) {
     return twisted_kernel_impl(bw, std::make_integer_sequence<int, kBandMax + 1>{});
 }
+static_assert(band_lds_doubles(kBandMax, 1) * sizeof(double) <= 159 * 1024, "kBandMax window must fit LDS");
 inline int band_ring(int bw, int nf) {
     const size_t budget = 150 * 1024, base = band_lds_bytes(bw);
     const size_t per = sizeof(double) * ((size_t)bw * 36 + 36 + 6);
@@ -334,7 +335,7 @@ inline int band_ring(int bw, int nf) {
 }
 inline size_t band_lds_bytes(int bw, int nf) { return sizeof(double) * band_lds_doubles(bw, band_ring(bw, nf)); }
 inline size_t twisted_lds_bytes(int bw, int nf) {
-    return band_lds_bytes(bw, nf) + sizeof(double) * (twisted_extra_doubles(bw) + (size_t)nf * 6);  // + x_p staging
+    return std::max(band_lds_bytes(bw, nf), sizeof(double) * (twisted_merge_doubles(bw) + (size_t)nf * 6));  // + x_p staging
 }
 template <int... B>
 const void *cl_kernel_impl(int bw, bool twisted, std::integer_sequence<int, B...>) {
@@ -429,9 +430,9 @@ struct SpecChoice {
 // trial slots of a BCR window run side by side only if they all fit (else the second slot's
 // super-rows would wait for the first's to retire and the levels would serialise). A/B at C4
 // (DESIGN §2): 1,551 -> 1,817 LM it/s (31 -> 22 steps per LBA); PLBA_SPEC_BCR=0 disables.
-inline SpecChoice spec_choice(bool cl, bool bcr, int bcr_fit, bool sharded, bool has_trials) {
+inline SpecChoice spec_choice(bool band1, bool bcr, int bcr_fit, bool sharded, bool has_trials) {
     SpecChoice r{1, kSpecOff};
-    if (sharded || !has_trials || !(cl || bcr)) return r;
+    if (sharded || !has_trials || !(band1 || bcr)) return r;
     int cap = kMaxSpec;
     if (bcr) {
         const char *b = getenv("PLBA_SPEC_BCR");
@@ -463,8 +464,8 @@ inline hipError_t launch_band(Dev &d, hipStream_t s) {
         return hipLaunchKernel(k, dim3(d.twisted ? 2 : 1, d.spec_max), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
     }
     if (d.twisted)
-        return hipLaunchKernel(twisted_kernel(d.bw), dim3(2), dim3(kBandNT), args, twisted_lds_bytes(d.bw, d.nf), s);
-    return hipLaunchKernel(band_kernel(d.bw), dim3(1), dim3(kBandNT), args, band_lds_bytes(d.bw, d.nf), s);
+        return hipLaunchKernel(twisted_kernel(d.bw), dim3(2, d.spec_max), dim3(kBandNT), args, twisted_lds_bytes(d.bw, d.nf), s);
+    return hipLaunchKernel(band_kernel(d.bw), dim3(1, d.spec_max), dim3(kBandNT), args, band_lds_bytes(d.bw, d.nf), s);
 }
 
 // time a launch when kernel timing is enabled
@@ -1048,12 +1049,12 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.tw_m = twisted ? tw_split(nf, bw) : 0;
     d.corrected = ctx->opts.corrected_line_jacobian;
     // Speculative trials: worth it where the step is bound by the serial factorisation
-    // chain and the rest of the chip idles during it — the column-lane factorisation (one or two
-    // workgroups per trial) and BCR windows whose slots' super-rows all fit the device at once;
+    // chain and the rest of the chip idles during it — the banded one- or two-workgroup
+    // factorisations (column-lane, LDS window) and BCR windows whose slots' super-rows all fit the device at once;
     // the extra slots' edge and landmark kernels are then the price. Not for the dense path or
     // sharded windows (collectives per slot).
     {
-        const SpecChoice sp = spec_choice(d.cl != 0, bcr, bcr ? bcr_res / std::max(d.bcr_N, 1) : 0, sharded,
+        const SpecChoice sp = spec_choice(band_mode && !bcr, bcr, bcr ? bcr_res / std::max(d.bcr_N, 1) : 0, sharded,
                                           n_lm > 0 && nch > 0);
         d.spec_max = sp.slots;
         d.spec_policy = sp.policy;

@@ -44,7 +44,7 @@ constexpr int kLmBlock = 64;  // landmark-parallel kernels: 24k landmarks at C3 
 constexpr int kChunk = PLBA_CHUNK;  // Schur triples per assembly wave (4 per lane)
 constexpr int kTraceCap = 64;
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
-constexpr int kBandMax = 20; // widest envelope (in pose blocks) the LDS-window factorisation holds
+constexpr int kBandMax = 28; // widest envelope (in pose blocks) the LDS-window factorisation holds
 #ifndef PLBA_BAND_NT
 #define PLBA_BAND_NT 1024
 #endif
@@ -1768,40 +1768,59 @@ struct BandSeg {
     double *sep;               // nullable: [BW][BW+1][36] + [BW][6]
 };
 
+// Diagonal-major ring window. Block (i, i-w) of a live row lives in diagonal w's ring of
+// C_w = W-w+1 slots, at slot i mod C_w. At step k diagonal w holds rows k+w..k+BW (its W-w
+// blocks in columns >= k) plus one spare slot — row k+w-1's, whose column k-1 is eliminated —
+// which the entering row k+W takes during step k while column k is still being read. That is
+// W(W+3)/2 blocks instead of the W² of a row-slot ring (bw 20: 252 vs 441; bw 28: 464 vs 841),
+// which is what lets bandwidths up to kBandMax sit in LDS.
+__host__ __device__ constexpr int bd_cap(int W, int w) { return W - w + 1; }
+__host__ __device__ constexpr int bd_base(int W, int w) { return w * (W + 1) - w * (w - 1) / 2; }
+__host__ __device__ constexpr int bd_blocks(int W) { return W * (W + 3) / 2; }
+// slot counter that advances with the row index (no runtime modulo in the step loop)
+struct BdPos {
+    int p, c;
+    __device__ __forceinline__ void step() { p = (p + 1 == c) ? 0 : p + 1; }
+};
+
 template <int BW>
 __device__ __forceinline__ void band_lds(double *lds, int R, double *&win, double *&bwin, double *&Lcol, double *&Kv,
                                          double *&xr, double *&part, double *&ys, double *&ringL, double *&ringK,
                                          double *&ringZ) {
     constexpr int W = BW + 1;
-    win = lds;                            // [W slots][W][36]
-    bwin = win + (size_t)W * W * 36;      // [W][6]
-    Lcol = bwin + (size_t)W * 6;          // [W][36]  (index w = 1..BW)
-    Kv = Lcol + (size_t)W * 36;           // [2][36]  S_k^{-1} double buffer
-    xr = Kv + 72;                         // [W][6]  ring of solved x blocks
-    part = xr + (size_t)W * 6;            // [W][6]
-    ys = part + (size_t)W * 6;            // [2][6]  y_k snapshots
-    ringL = ys + 12;                      // [R][BW][36]
-    ringK = ringL + (size_t)R * BW * 36;  // [R+1][36]
-    ringZ = ringK + (size_t)(R + 1) * 36; // [R+1][6]
+    win = lds;                                   // [bd_blocks(W)][36] diagonal rings
+    bwin = win + (size_t)bd_blocks(W) * 36;      // [W][6]  right-hand sides, row slot ring
+    Lcol = bwin + (size_t)W * 6;                 // [W][36]  (index w = 1..BW)
+    Kv = Lcol + (size_t)W * 36;                  // [2][36]  S_k^{-1} double buffer
+    xr = Kv + 72;                                // [W][6]  ring of solved x blocks
+    part = xr + (size_t)W * 6;                   // [W][6]
+    ys = part + (size_t)W * 6;                   // [2][6]  y_k snapshots
+    ringL = ys + 12;                             // [R][BW][36]
+    ringK = ringL + (size_t)R * BW * 36;         // [R+1][36]
+    ringZ = ringK + (size_t)(R + 1) * 36;        // [R+1][6]
 }
-// doubles of the band layout above, and of the twisted kernel's extra regions behind it
+// doubles of the band layout above
 __host__ __device__ constexpr size_t band_lds_doubles(int bw, int R) {
-    return (size_t)(bw + 1) * (bw + 1) * 36 + (size_t)(bw + 1) * (6 + 36 + 6 + 6) + 72 + 12 + (size_t)R * bw * 36 +
+    return (size_t)bd_blocks(bw + 1) * 36 + (size_t)(bw + 1) * (6 + 36 + 6 + 6) + 72 + 12 + (size_t)R * bw * 36 +
            (size_t)(R + 1) * 42;
 }
-__host__ __device__ constexpr size_t twisted_extra_doubles(int bw) {
-    return 2 * (size_t)(bw + 1) * 6 + (size_t)(6 * bw) * (6 * bw + 1) + 72 * (size_t)bw;
+// The twisted kernel's merge, after both segments have exported their separator windows, reuses
+// the LDS from 0: Ms [6bw][6bw+1], pivot inverses + factors [2][bw][36], two backward rings
+// xr/part [4][bw+1][6]; then the x_p staging [nf][6].
+__host__ __device__ constexpr size_t twisted_merge_doubles(int bw) {
+    return (size_t)(6 * bw) * (6 * bw + 1) + 72 * (size_t)bw + 24 * (size_t)(bw + 1);
 }
 
 template <int BW>
 __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int ring, unsigned long long *stamps) {
     constexpr int NT = kBandNT, W = BW + 1, NW = NT - 64;
     constexpr int NPAIR = BW * (BW + 1) / 2;             // trailing (wi >= wj >= 1) block pairs
-    constexpr int PPT0 = (NPAIR * 36 - 36 + NW - 1) / NW; // pair entries per worker (pair 0 = wave 0)
-    constexpr int PPT = PPT0 > 0 ? PPT0 : 1;
+    // trailing-update units: half blocks (3 rows x 6 columns) of every pair but (1,1), which is
+    // wave 0's; a unit reads its 3 L rows, the 6x6 column block A_jk and its 18 targets once
+    constexpr int NU = 2 * (NPAIR - 1);
+    constexpr int UPT = NU > 0 ? (NU + NW - 1) / NW : 1;  // units per worker
     constexpr int LPT = ((BW > 1 ? BW - 1 : 0) * 36 + NW - 1) / NW;  // L entries per worker (w >= 2)
     constexpr int RFT = (W * 36 + NW - 1) / NW;           // refill entries per worker
-    constexpr int NPT = (NPAIR * 36 > 36) ? NPAIR * 36 : 36; // valid pair-entry bound
     const int nrows = g.nrows, nsteps = g.nsteps;
     double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
     band_lds<BW>(lds, ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
@@ -1813,33 +1832,55 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     const bool crit = tid < 64;                   // wave 0
     const int wt = tid - 64;                      // worker thread index
     if (tid == 0) s_fail = 0;
+    // rows 0..BW: block (r, r-w), w <= r, to diagonal w's slot r mod C_w
     for (int t = tid; t < W * W * 36; t += NT) {
-        const int row = t / (W * 36), rem = t % (W * 36);
-        win[t] = (row < nrows) ? g.Bd[((size_t)row * W) * 36 + rem] : 0.0;
+        const int r = t / (W * 36), rem = t % (W * 36), w = rem / 36;
+        if (w <= r)
+            win[(size_t)(bd_base(W, w) + r % bd_cap(W, w)) * 36 + rem % 36] =
+                (r < nrows) ? g.Bd[((size_t)r * W) * 36 + rem] : 0.0;
     }
     for (int t = tid; t < W * 6; t += NT) bwin[t] = (t / 6 < nrows) ? g.bs[t] : 0.0;
-    // ---- per-worker static assignment
-    int p_wi[PPT], p_wj[PPT], p_li[PPT], p_aj[PPT], p_dst[PPT];
+    // ---- per-worker static assignment; slot counters start at step 0
+    int u_wi[UPT], u_wj[UPT], u_h[UPT], u_bt[UPT], u_ba[UPT];
+    BdPos u_pt[UPT], u_pa[UPT];
 #pragma unroll
-    for (int q = 0; q < PPT; ++q) {
-        const int t = wt + 36 + q * NW;
-        int pr = t / 36, e = t % 36, wi = 1;
+    for (int q = 0; q < UPT; ++q) {
+        const int u = wt + q * NW;
+        const bool ok = !crit && u < NU;
+        const int pr = 1 + (ok ? u / 2 : 0);
+        int wi = 1;
         while ((wi * (wi + 1)) / 2 <= pr) ++wi;
         const int wj = pr - (wi - 1) * wi / 2 + 1;
-        const bool ok = !crit && t < NPT && NPAIR > 1;
-        p_wi[q] = ok ? wi : 1 << 20;               // never <= wmax when invalid
-        p_wj[q] = wj;
-        p_li[q] = wi * 36 + (e / 6) * 6;
-        p_aj[q] = wj * 36 + (e % 6) * 6;
-        p_dst[q] = (wi - wj) * 36 + e;
+        u_wi[q] = ok ? wi : 1 << 20;               // never <= wmax when invalid
+        u_wj[q] = wj;
+        u_h[q] = (u & 1) * 18;
+        u_bt[q] = bd_base(W, wi - wj);             // target (k+wi, k+wj): diagonal wi-wj, row k+wi
+        u_pt[q] = BdPos{wi % bd_cap(W, wi - wj), bd_cap(W, wi - wj)};
+        u_ba[q] = bd_base(W, wj);                  // A_jk = (k+wj, k): diagonal wj, row k+wj
+        u_pa[q] = BdPos{wj % bd_cap(W, wj), bd_cap(W, wj)};
     }
-    int l_w[LPT > 0 ? LPT : 1], l_e[LPT > 0 ? LPT : 1];
+    int l_w[LPT > 0 ? LPT : 1], l_e[LPT > 0 ? LPT : 1], l_b[LPT > 0 ? LPT : 1];
+    BdPos l_p[LPT > 0 ? LPT : 1];
 #pragma unroll
     for (int q = 0; q < LPT; ++q) {
         const int t = wt + 36 + q * NW;
-        l_w[q] = (!crit && t < BW * 36) ? 1 + t / 36 : 1 << 20;
+        const bool ok = !crit && t < BW * 36;
+        const int w = ok ? 1 + t / 36 : 1;
+        l_w[q] = ok ? w : 1 << 20;
         l_e[q] = t % 36;
+        l_b[q] = bd_base(W, w);                    // A_{k+w,k}: diagonal w, row k+w
+        l_p[q] = BdPos{w % bd_cap(W, w), bd_cap(W, w)};
     }
+    int r_dst[RFT];                                // refill: row k+W, block w = t/36
+    BdPos r_p[RFT];
+#pragma unroll
+    for (int q = 0; q < RFT; ++q) {
+        const int t = min(max(wt, 0) + q * NW, W * 36 - 1), w = t / 36;
+        r_dst[q] = bd_base(W, w) * 36 + t % 36;
+        r_p[q] = BdPos{W % bd_cap(W, w), bd_cap(W, w)};
+    }
+    BdPos c_p0{1 % bd_cap(W, 0), bd_cap(W, 0)}, c_p1{1 % bd_cap(W, 1), bd_cap(W, 1)};  // row k+1, diag 0 / 1
+    constexpr int cb1 = bd_base(W, 1);
     double pf[RFT], pfn[RFT];
     double pfb = 0.0, pfbn = 0.0;
     auto prefetch = [&](int row, double (&dst)[RFT], double &dstb) {
@@ -1855,7 +1896,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     if (crit) {
         bool fail = false;
         double M = 0.0;
-        if (lane < 36) M = win[lane];
+        if (lane < 36) M = win[lane];              // block (0, 0): diagonal 0, slot 0
         else if (lane < 42) { M = bwin[lane - 36]; ys[lane - 36] = M; }
         const double I = gj_inverse6(M, lane, fail);
         if (lane < 36) { Kv[lane] = I; ringK[lane] = I; }
@@ -1868,7 +1909,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     unsigned long long st_last;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
-    int sk = 0, kR = 0, kRK = 1;                  // k % W, k % R, (k+1) % RK
+    int sk = 0, kR = 0, kRK = 1;                  // k % W (rhs row slots), k % R, (k+1) % RK
     // a zero pivot sets s_fail and the sweep runs on (inf/NaN blocks are never used: the
     // caller drops the solve); no per-step LDS read of the flag on the critical chain
     for (int k = 0; k < nsteps; ++k) {
@@ -1888,7 +1929,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         if (crit) {
             if (lane < 36 && wmax >= 1) {
                 const int c = lane % 6;
-                const double *Aik = win + ((size_t)slot(1) * W + 1) * 36 + (lane / 6) * 6;
+                const double *Aik = win + (size_t)(cb1 + c_p1.p) * 36 + (lane / 6) * 6;
                 double v = 0.0;
 #pragma unroll
                 for (int m = 0; m < 6; ++m) v = fma(Aik[m], Kk[m * 6 + c], v);
@@ -1900,7 +1941,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
             for (int q = 0; q < LPT; ++q) {
                 const int w = l_w[q], e = l_e[q];
                 if (w <= wmax) {
-                    const double *Aik = win + ((size_t)slot(w) * W + w) * 36 + (e / 6) * 6;
+                    const double *Aik = win + (size_t)(l_b[q] + l_p[q].p) * 36 + (e / 6) * 6;
                     const int c = e % 6;
                     double v = 0.0;
 #pragma unroll
@@ -1926,11 +1967,11 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                     double sacc = 0.0;
                     if constexpr (BW >= 1) {
                         const double *L1 = Lcol + 36 + r * 6;
-                        const double *A1 = mat ? win + ((size_t)s1 * W + 1) * 36 + c * 6 : yk;
+                        const double *A1 = mat ? win + (size_t)(cb1 + c_p1.p) * 36 + c * 6 : yk;
 #pragma unroll
                         for (int m = 0; m < 6; ++m) sacc = fma(L1[m], A1[m], sacc);
                     }
-                    double *dst = mat ? win + ((size_t)s1 * W + 0) * 36 + lane : bwin + s1 * 6 + r;
+                    double *dst = mat ? win + (size_t)c_p0.p * 36 + lane : bwin + s1 * 6 + r;
                     M = *dst - sacc;
                     *dst = M;
                     if (!mat) ys[k1b * 6 + r] = M;
@@ -1943,17 +1984,36 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                 if (fail && lane == 0 && k + 1 < nsteps) s_fail = 1;
             }
         } else {
-            // trailing update A_ij -= L_ik A_jkᵀ for all pairs (wi >= wj >= 1) except (1,1)
+            // trailing update A_ij -= L_ik A_jkᵀ for all pairs (wi >= wj >= 1) except (1,1), three
+            // target rows per unit (same fma order per entry as one entry at a time)
 #pragma unroll
-            for (int q = 0; q < PPT; ++q) {
-                const int wi = p_wi[q];
-                if (wi <= wmax) {
-                    const double *Li = Lcol + p_li[q];
-                    const double *Ajk = win + (size_t)slot(p_wj[q]) * W * 36 + p_aj[q];
-                    double sacc = 0.0;
+            for (int q = 0; q < UPT; ++q) {
+                if (u_wi[q] <= wmax) {
+                    const double2 *Li = (const double2 *)(Lcol + u_wi[q] * 36 + u_h[q]);
+                    const double2 *Aj = (const double2 *)(win + (size_t)(u_ba[q] + u_pa[q].p) * 36);
+                    double2 *T = (double2 *)(win + (size_t)(u_bt[q] + u_pt[q].p) * 36 + u_h[q]);
+                    double l[18];
 #pragma unroll
-                    for (int m = 0; m < 6; ++m) sacc = fma(Li[m], Ajk[m], sacc);
-                    win[(size_t)slot(wi) * W * 36 + p_dst[q]] -= sacc;
+                    for (int v = 0; v < 9; ++v) { const double2 x = Li[v]; l[2 * v] = x.x; l[2 * v + 1] = x.y; }
+#pragma unroll
+                    for (int c = 0; c < 6; c += 2) {  // target columns c, c+1: rows c, c+1 of A_jk
+                        double a[12];
+#pragma unroll
+                        for (int v = 0; v < 6; ++v) { const double2 x = Aj[c * 3 + v]; a[2 * v] = x.x; a[2 * v + 1] = x.y; }
+#pragma unroll
+                        for (int r = 0; r < 3; ++r) {
+                            double2 t = T[r * 3 + c / 2];
+                            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                            for (int m = 0; m < 6; ++m) {
+                                s0 = fma(l[r * 6 + m], a[m], s0);
+                                s1 = fma(l[r * 6 + m], a[6 + m], s1);
+                            }
+                            t.x -= s0;
+                            t.y -= s1;
+                            T[r * 3 + c / 2] = t;
+                        }
+                    }
                 }
             }
             STAMP(5);
@@ -1983,12 +2043,12 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                 for (int t = wt; t < cnt * 6; t += NW) g.zb[(size_t)k0 * 6 + t] = ringZ[((k0 + t / 6) % RK) * 6 + t % 6];
             }
             STAMP(7);
-            // block row k+W enters slot sk (row k is fully consumed)
+            // block row k+W enters: diagonal w's spare slot (row k+w-1's, column k-1 eliminated)
             const bool live = k + W < nrows;
 #pragma unroll
             for (int q = 0; q < RFT; ++q) {
                 const int t = wt + q * NW;
-                if (t < W * 36) win[(size_t)sk * W * 36 + t] = live ? pf[q] : 0.0;
+                if (t < W * 36) win[(size_t)r_p[q].p * 36 + r_dst[q]] = live ? pf[q] : 0.0;
             }
             if (wt < 6) bwin[sk * 6 + wt] = live ? pfb : 0.0;
         }
@@ -1998,6 +2058,14 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         sk = (sk + 1 == W) ? 0 : sk + 1;
         kR = (kR + 1 == R) ? 0 : kR + 1;
         kRK = (kRK + 1 == RK) ? 0 : kRK + 1;
+        c_p0.step();
+        c_p1.step();
+#pragma unroll
+        for (int q = 0; q < UPT; ++q) { u_pt[q].step(); u_pa[q].step(); }
+#pragma unroll
+        for (int q = 0; q < LPT; ++q) l_p[q].step();
+#pragma unroll
+        for (int q = 0; q < RFT; ++q) r_p[q].step();
     }
 #ifdef PLBA_STAMPS
     if (stamps && (tid & 63) == 0)
@@ -2005,10 +2073,10 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
 #endif
     __syncthreads();  // drains every wave's flush stores: the backward pass reads them
     const bool failed = s_fail != 0;
-    if (g.sep && !failed) {  // rows nsteps..nsteps+BW-1 (all W blocks) and their right-hand sides
+    if (g.sep && !failed) {  // rows nsteps..nsteps+BW-1 (all W blocks; eliminated columns as 0) and their right-hand sides
         for (int t = tid; t < BW * W * 36; t += NT) {
-            const int i = t / (W * 36), rem = t % (W * 36);
-            g.sep[t] = win[(size_t)((sk + i) % W) * W * 36 + rem];
+            const int i = t / (W * 36), rem = t % (W * 36), w = rem / 36, r = nsteps + i;
+            g.sep[t] = w <= i ? win[(size_t)(bd_base(W, w) + r % bd_cap(W, w)) * 36 + rem % 36] : 0.0;
         }
         for (int t = tid; t < BW * 6; t += NT) g.sep[(size_t)BW * W * 36 + t] = bwin[((sk + t / 6) % W) * 6 + t % 6];
     }
@@ -2157,10 +2225,10 @@ __device__ __forceinline__ void band_backward(const double *Lband, const double 
 
 template <int BW>
 __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d0) {
-    TRIAL_SLOT(0)
+    TRIAL_SLOT(blockIdx.y)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const BandSeg g{d.Bd, d.bs, d.Lband, d.Kinv, d.zb, d.nf, d.nf, nullptr};
-    const bool fail = band_forward<BW>(g, lds, d.ring, d.stamps);
+    const bool fail = band_forward<BW>(g, lds, d.ring, d.stamps) || diag_fail(d);
     if (threadIdx.x == 0) *d.solve_okp = fail ? 0 : 1;
     if (!fail && threadIdx.x < 64) {
         double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
@@ -2192,7 +2260,7 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
 #ifdef PLBA_STAMPS
     unsigned long long tw_t0 = __builtin_readcyclecounter();
 #endif
-    const bool fail = band_forward<BW>(g, lds, d.ring, seg == 0 ? d.stamps : nullptr);
+    const bool fail = band_forward<BW>(g, lds, d.ring, seg == 0 ? d.stamps : nullptr) || diag_fail(d);
 #ifdef PLBA_STAMPS
     unsigned long long tw_t1 = __builtin_readcyclecounter();
 #define TW_MARK(q, t)                                                     \
@@ -2225,11 +2293,11 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
     __syncthreads();
     if (!s_last) return;
     if (!s_sfail) {
-    double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
-    band_lds<BW>(lds, d.ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
-    double *xr1 = lds + band_lds_doubles(BW, d.ring), *part1 = xr1 + W * 6;
-    double *Ms = part1 + W * 6, *fcol = Ms + (size_t)NS * LD;
-    double *xl = lds + band_lds_doubles(BW, d.ring) + twisted_extra_doubles(BW);  // [nf][6] x_p staging
+    // merge layout (twisted_merge_doubles) from LDS offset 0: the band windows are dead, both
+    // separators having been exported to global memory before the arrival
+    double *Ms = lds, *fcol = Ms + (size_t)NS * LD;
+    double *xr = fcol + 72 * BW, *part = xr + W * 6, *xr1 = part + W * 6, *part1 = xr1 + W * 6;
+    double *xl = lds + twisted_merge_doubles(BW);  // [nf][6] x_p staging
     // ---- separator system S_sep (lower block (i,j), i >= j, w = i-j) and its right-hand side
     const double *W0 = d.tw_sep, *W1 = d.tw_sep + sep_stride;
     for (int t = tid; t < NS * NS; t += NT) {
@@ -2331,7 +2399,7 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
 template <int BW>
 __global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d0) {
     if constexpr (BW >= 1) {  // (the host never selects bw 0)
-        TRIAL_SLOT(0)
+        TRIAL_SLOT(blockIdx.y)
         k_rcs_factor_twisted_body<BW>(d);
     }
 }

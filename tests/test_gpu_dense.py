@@ -74,6 +74,7 @@ def test_dense_mfma_factorisation(solver, monkeypatch, cfg, kw):
     workgroups with v_mfma_f64_16x16x4 trailing updates, and the scalar single-workgroup kernel,
     both against the oracle."""
     monkeypatch.setenv("PLBA_NO_RCM", "1")
+    monkeypatch.setenv("PLBA_FORCE_DENSE", "1")  # (the 30-KF window's bw 26 is banded otherwise)
     g = synth.generate(cfg, **kw)
     ref = oa.lba_plucker(g)
     solver.upload(g)
@@ -89,11 +90,24 @@ def test_dense_mfma_factorisation(solver, monkeypatch, cfg, kw):
     assert np.abs(mf["kf_Tcw"] - sc["kf_Tcw"]).max() < 1e-9
 
 
+def test_revisit_window_wide_band(solver):
+    """C3R: the loop revisit folds (RCM) into a band of 23 pose blocks — wider than the 20 a
+    row-slot LDS window holds — so it runs the diagonal-ring window of k_rcs_factor_band
+    (bw 21..28) instead of the dense path; parity with the oracle."""
+    g = synth.generate("C3R")
+    ref = oa.lba_plucker(g)
+    solver.upload(g)
+    st = solver.structure_stats()
+    assert st["banded"] == 1 and 20 < st["bw"] <= 28 and st["dense_mfma"] == 0, st
+    _check(solver.lba_plucker(), ref)
+
+
 def test_dense_mfma_hand_rolled_lm(solver, monkeypatch):
     """The hand-rolled LM (plba_hlm_lba) through the dense path."""
     from plba import capi
     from plba.hlm import hlm_window
     monkeypatch.setenv("PLBA_NO_RCM", "1")
+    monkeypatch.setenv("PLBA_FORCE_DENSE", "1")
     win = hlm_window(synth.generate("C1", n_kf=30, n_pt=400, seed=35, track_max=30))
     p = capi.hlm_params(err_per_obs=1)
     ref = oa.hlm_lba(win, p)
@@ -110,6 +124,7 @@ def test_dense_solve_with_y_in_global_memory(solver, monkeypatch):
     PLBA_SOLVE_LDS_N=0 takes that path at a size the oracle finishes. Same operations in the same
     order as the LDS path, so the two agree bitwise."""
     monkeypatch.setenv("PLBA_NO_RCM", "1")
+    monkeypatch.setenv("PLBA_FORCE_DENSE", "1")
     g = synth.generate("C1", n_kf=30, n_pt=400, seed=35, track_max=30)
     ref = oa.lba_plucker(g)
     solver.upload(g)

@@ -95,14 +95,20 @@ def test_shuffled_edges_and_ids(solver):
     assert np.abs(out["pt_xyz"] - base["pt_xyz"][pp]).max() < 1e-8
 
 
-@pytest.mark.parametrize("tmax,n_kf", [(12, 24), (30, 30)])
-def test_wide_bands_and_dense_fallback(solver, tmax, n_kf):
-    # tmax 12 -> banded kernel with bw 11; tmax 30 -> envelope wider than kBandMax (dense path)
+@pytest.mark.parametrize("tmax,n_kf,banded", [(12, 24, 1), (30, 30, 1), (60, 60, 0)])
+def test_wide_bands_and_dense_fallback(solver, monkeypatch, tmax, n_kf, banded):
+    # tmax 12 -> banded kernel with bw 11; tmax 30 -> bw 21, the diagonal-ring LDS window
+    # (bw 21..kBandMax = 28); the 60-KF window with scrambled keyframe ids and no reordering ->
+    # an envelope wider than kBandMax (dense path)
     g = synth.generate("C1", n_kf=n_kf, n_pt=400, seed=5 + tmax, track_min=2, track_max=tmax, fixed_frac=0.1)
+    if not banded:
+        g = g.copy()
+        g.kf_id = np.random.default_rng(3).permutation(g.n_kf).astype(np.int32)
+        monkeypatch.setenv("PLBA_NO_RCM", "1")
     out, ref = _run(solver, g)
     _check(out, ref)
     st = solver.structure_stats()
-    assert st["banded"] == (1 if tmax <= 20 else 0), st
+    assert st["banded"] == banded and (st["bw"] <= 28) == bool(banded), st
 
 
 @pytest.mark.parametrize("cfg,kw", [("C2", {}), ("C1", dict(n_kf=60, n_pt=1500, seed=77, track_max=12))])

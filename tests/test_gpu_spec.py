@@ -138,6 +138,24 @@ def test_speculative_slots_on_block_cyclic_reduction_are_bitwise(cfg):
                 assert st["device_steps"] <= st0["device_steps"], (st, st0)
 
 
+@pytest.mark.parametrize("cfg,kw", [("C2R", {}), ("C1", dict(n_kf=30, n_pt=400, seed=35, track_max=30))])
+def test_speculative_slots_on_the_lds_window_band_kernel_are_bitwise(cfg, kw):
+    """Trial slots on the LDS-window band kernels (grid.y = slot; per-slot band, factors and
+    separator windows): C2R runs the two-sided kernel at bw 20, the 30-KF window the one-sided
+    diagonal-ring window at bw 26. Bitwise the one-slot solve, with forced solve failures too."""
+    g = synth.generate(cfg, **kw)
+    for diag in (0, 128):
+        base, base2, st0 = _solve(g, 1, 0, diag=diag)
+        assert st0["banded"] == 1 and st0["column_lane"] == 0 and st0["bcr_rows"] == 0, st0
+        _assert_same(base, base2, "rerun")
+        for slots, pol in ((2, 1), (3, 3), (4, 2)):
+            out, out2, st = _solve(g, slots, pol, diag=diag)
+            assert st["spec_slots"] == slots, st
+            _assert_same(base, out, (slots, pol, diag))
+            _assert_same(base, out2, (slots, pol, diag, "second schedule"))
+            assert st["device_steps"] <= st0["device_steps"], (st, st0)
+
+
 def test_speculative_zero_pivot_window():
     """τ = 0 and a keyframe with zero information: every solve fails (λ stays 0), every slot's
     trial is rejected with the previous x and optimize(5) terminates after maxTrials."""
