@@ -530,7 +530,10 @@ def main():
                 "upload_ms": upload_ms,
                 "end_to_end": e2e[-1],
                 "factorisation": ("block cyclic reduction over %d super-rows" % info["bcr_rows"] if info.get("bcr_rows")
-                                  else ("two-sided column-lane band LDLT" if info.get("twisted") else "band LDLT")),
+                                  else "dense blocked LDLT (MFMA)" if not info.get("banded")
+                                  else "%s%s band LDLT (bw %d)" % ("two-sided " if info.get("twisted") else "",
+                                                                   "column-lane" if info.get("column_lane") else "register-window",
+                                                                   info.get("bw", 0))),
                 "speculative_trials": {"slots": info.get("spec_slots", 1), "policy": info.get("spec_policy", 0),
                                        "device_steps_per_lba": info.get("device_steps")},
                 "parallelism": (f"landmark-sharded window over {world} GPU(s)" if shard

@@ -326,9 +326,10 @@ const void *twisted_kernel_impl(int bw, std::integer_sequence<int, B...>) {
 inline const void *twisted_kernel(int bw) {
     return twisted_kernel_impl(bw, std::make_integer_sequence<int, kBandMax + 1>{});
 }
-static_assert(band_lds_doubles(kBandMax, 1) * sizeof(double) <= 159 * 1024, "kBandMax window must fit LDS");
+static_assert(band_lds_doubles(kBandMax, 1) * sizeof(double) + band_static_bytes(kBandMax) <= 158 * 1024,
+              "kBandMax window must fit LDS");
 inline int band_ring(int bw, int nf) {
-    const size_t budget = 150 * 1024, base = band_lds_bytes(bw);
+    const size_t budget = 158 * 1024 - band_static_bytes(bw), base = band_lds_bytes(bw);
     const size_t per = sizeof(double) * ((size_t)bw * 36 + 36 + 6);
     int R = base + per < budget ? (int)((budget - base - per) / per) : 1;
     return std::max(1, std::min(R, 16));
@@ -430,7 +431,7 @@ struct SpecChoice {
 // trial slots of a BCR window run side by side only if they all fit (else the second slot's
 // super-rows would wait for the first's to retire and the levels would serialise). A/B at C4
 // (DESIGN §2): 1,551 -> 1,817 LM it/s (31 -> 22 steps per LBA); PLBA_SPEC_BCR=0 disables.
-inline SpecChoice spec_choice(bool band1, bool bcr, int bcr_fit, bool sharded, bool has_trials) {
+inline SpecChoice spec_choice(bool band1, bool wide, bool bcr, int bcr_fit, bool sharded, bool has_trials) {
     SpecChoice r{1, kSpecOff};
     if (sharded || !has_trials || !(band1 || bcr)) return r;
     int cap = kMaxSpec;
@@ -439,7 +440,9 @@ inline SpecChoice spec_choice(bool band1, bool bcr, int bcr_fit, bool sharded, b
         if ((b && b[0] == '0') || bcr_fit < 2) return r;
         cap = std::min(cap, bcr_fit);
     }
-    r.slots = 2;
+    // wide bands (bw > 9: the register-window kernel, ≈0.5 ms a factorisation at C3R) take every
+    // slot: C3R 21 -> 17 steps per LBA, 1,000 -> 1,194 LM it/s (2 / 3 / 4 slots)
+    r.slots = wide ? kMaxSpec : 2;
     r.policy = kSpecSticky;
     const char *e = getenv("PLBA_SPEC");
     if (e && e[0]) r.slots = std::max(1, std::min(atoi(e), kMaxSpec));
@@ -1033,7 +1036,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     d.bcr_N = bcr ? (nf + bw - 1) / bw : 0;
     const bool cl = band_mode && !bcr && use_cl(bw);
     const bool twisted = band_mode && !bcr && bw >= 1 && nf >= 2 * bw + 16 &&
-                         (cl ? cl_lds_bytes(bw, nf, true) : twisted_lds_bytes(bw, nf)) <= 159 * 1024 &&
+                         (cl ? cl_lds_bytes(bw, nf, true) : twisted_lds_bytes(bw, nf) + band_static_bytes(bw)) <= 159 * 1024 &&
                          !(no_twist && no_twist[0] == '1');
     // the column-lane factorisation a BCR window falls back to (run_schedule) and its arrays
     // (the same checks as the normal column-lane choice; without it, the one-sweep band kernel)
@@ -1054,7 +1057,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     // the extra slots' edge and landmark kernels are then the price. Not for the dense path or
     // sharded windows (collectives per slot).
     {
-        const SpecChoice sp = spec_choice(band_mode && !bcr, bcr, bcr ? bcr_res / std::max(d.bcr_N, 1) : 0, sharded,
+        const SpecChoice sp = spec_choice(band_mode && !bcr, band_mode && !bcr && !d.cl, bcr, bcr ? bcr_res / std::max(d.bcr_N, 1) : 0, sharded,
                                           n_lm > 0 && nch > 0);
         d.spec_max = sp.slots;
         d.spec_policy = sp.policy;

@@ -44,11 +44,14 @@ constexpr int kLmBlock = 64;  // landmark-parallel kernels: 24k landmarks at C3 
 constexpr int kChunk = PLBA_CHUNK;  // Schur triples per assembly wave (4 per lane)
 constexpr int kTraceCap = 64;
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
-constexpr int kBandMax = 28; // widest envelope (in pose blocks) the LDS-window factorisation holds
+constexpr int kBandMax = 24; // widest envelope (in pose blocks) the register-window factorisation holds
 #ifndef PLBA_BAND_NT
-#define PLBA_BAND_NT 1024
+#define PLBA_BAND_NT 768
 #endif
 constexpr int kBandNT = PLBA_BAND_NT; // threads of the banded factorisation workgroup
+// rows of a band block one worker owns in registers (plba_kernels.hpp band_forward): whole 6x6
+// blocks at 512 threads (256 VGPRs), half blocks when more, smaller waves are configured
+constexpr int kBandUR = kBandNT <= 512 ? 6 : 3;
 // Speculative trials (DESIGN §2 "Speculative trials"): a step may evaluate up to kMaxSpec damped
 // trials of one linearisation at once — λ, λ·ν, λ·ν·2ν, ... (exactly the λ sequence g2o's
 // Levenberg loop walks after rejections) — in trial slots 0..W-1 (blockIdx.y of the trial
@@ -1768,28 +1771,29 @@ struct BandSeg {
     double *sep;               // nullable: [BW][BW+1][36] + [BW][6]
 };
 
-// Diagonal-major ring window. Block (i, i-w) of a live row lives in diagonal w's ring of
-// C_w = W-w+1 slots, at slot i mod C_w. At step k diagonal w holds rows k+w..k+BW (its W-w
-// blocks in columns >= k) plus one spare slot — row k+w-1's, whose column k-1 is eliminated —
-// which the entering row k+W takes during step k while column k is still being read. That is
-// W(W+3)/2 blocks instead of the W² of a row-slot ring (bw 20: 252 vs 441; bw 28: 464 vs 841),
-// which is what lets bandwidths up to kBandMax sit in LDS.
+// Register-resident band window. Block (i, i-w) of a live row is owned by a pair of worker
+// threads (3 rows each) for its whole life in the window and updated in registers; it is written
+// to LDS once, when it becomes part of the next pivot column (the step's operand A_jk and the
+// source of L), or, on the diagonal, when it becomes the next pivot block. Ownership follows
+// diagonal-major rings: diagonal w has C_w = W-w+1 slots, row i in slot i mod C_w; at step k
+// the slot's offset o = (slot - k - w) mod C_w says which row it holds (i = k+w+o): o = 0 the
+// pivot column, 1 <= o <= BW-w a trailing block (pair wi = w+o, wj = o), o = C_w-1 the spare slot
+// that loads the entering row k+W from global memory during step k. W(W+3) half blocks
+// (bw 23: 648 of the 960 worker threads); LDS keeps only two pivot columns, the pivot blocks and
+// the L / S^-1 / z staging rings, so no read-modify-write of the trailing blocks goes through LDS.
 __host__ __device__ constexpr int bd_cap(int W, int w) { return W - w + 1; }
 __host__ __device__ constexpr int bd_base(int W, int w) { return w * (W + 1) - w * (w - 1) / 2; }
 __host__ __device__ constexpr int bd_blocks(int W) { return W * (W + 3) / 2; }
-// slot counter that advances with the row index (no runtime modulo in the step loop)
-struct BdPos {
-    int p, c;
-    __device__ __forceinline__ void step() { p = (p + 1 == c) ? 0 : p + 1; }
-};
 
 template <int BW>
-__device__ __forceinline__ void band_lds(double *lds, int R, double *&win, double *&bwin, double *&Lcol, double *&Kv,
-                                         double *&xr, double *&part, double *&ys, double *&ringL, double *&ringK,
-                                         double *&ringZ) {
+__device__ __forceinline__ void band_lds(double *lds, int R, double *&col, double *&piv, double *&bwin, double *&Lcol,
+                                         double *&Kv, double *&xr, double *&part, double *&ys, double *&ringL,
+                                         double *&ringK, double *&ringZ) {
     constexpr int W = BW + 1;
-    win = lds;                                   // [bd_blocks(W)][36] diagonal rings
-    bwin = win + (size_t)bd_blocks(W) * 36;      // [W][6]  right-hand sides, row slot ring
+    col = lds;                                   // [2][W][36] pivot columns k, k+1: block (c+w, c) at [c&1][w]
+    piv = col + (size_t)2 * W * 36;              // [2][36]  pivot block (c, c) at [c&1]
+    bwin = piv + 72;                             // [W][6]  right-hand sides, row slot ring
+    // (the entering rows are staged in band_forward's static LDS: band_static_bytes)
     Lcol = bwin + (size_t)W * 6;                 // [W][36]  (index w = 1..BW)
     Kv = Lcol + (size_t)W * 36;                  // [2][36]  S_k^{-1} double buffer
     xr = Kv + 72;                                // [W][6]  ring of solved x blocks
@@ -1801,29 +1805,31 @@ __device__ __forceinline__ void band_lds(double *lds, int R, double *&win, doubl
 }
 // doubles of the band layout above
 __host__ __device__ constexpr size_t band_lds_doubles(int bw, int R) {
-    return (size_t)bd_blocks(bw + 1) * 36 + (size_t)(bw + 1) * (6 + 36 + 6 + 6) + 72 + 12 + (size_t)R * bw * 36 +
+    return (size_t)(bw + 1) * 72 + 72 + (size_t)(bw + 1) * (6 + 36 + 6 + 6) + 72 + 12 + (size_t)R * bw * 36 +
            (size_t)(R + 1) * 42;
 }
+// static LDS of band_forward: the entering rows' staging buffers [2][W*36 + 6] (blocks, right-hand
+// side) plus a few flags. A separate LDS object from the dynamic window, so that the compiler can
+// tell the direct global->LDS loads into it from the window's reads (with one LDS object every
+// ds_read after such a load waits for it)
+__host__ __device__ constexpr size_t band_static_bytes(int bw) { return 16 * ((size_t)(bw + 1) * 36 + 6) + 64; }
 // The twisted kernel's merge, after both segments have exported their separator windows, reuses
-// the LDS from 0: Ms [6bw][6bw+1], pivot inverses + factors [2][bw][36], two backward rings
+// the LDS from 0: the separator system's packed lower triangle [6bw(6bw+1)/2], its right-hand side
+// and two solution copies [3][6bw], pivot inverses + one L column [2][bw][36], two backward rings
 // xr/part [4][bw+1][6]; then the x_p staging [nf][6].
 __host__ __device__ constexpr size_t twisted_merge_doubles(int bw) {
-    return (size_t)(6 * bw) * (6 * bw + 1) + 72 * (size_t)bw + 24 * (size_t)(bw + 1);
+    return (size_t)(6 * bw) * (6 * bw + 1) / 2 + 3 * (size_t)(6 * bw) + 72 * (size_t)bw + 24 * (size_t)(bw + 1);
 }
 
 template <int BW>
 __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int ring, unsigned long long *stamps) {
     constexpr int NT = kBandNT, W = BW + 1, NW = NT - 64;
-    constexpr int NPAIR = BW * (BW + 1) / 2;             // trailing (wi >= wj >= 1) block pairs
-    // trailing-update units: half blocks (3 rows x 6 columns) of every pair but (1,1), which is
-    // wave 0's; a unit reads its 3 L rows, the 6x6 column block A_jk and its 18 targets once
-    constexpr int NU = 2 * (NPAIR - 1);
-    constexpr int UPT = NU > 0 ? (NU + NW - 1) / NW : 1;  // units per worker
+    constexpr int UR = kBandUR, UPB = 6 / UR, UE = UR * 6;  // rows per owner, owners per block, entries
+    static_assert(UPB * bd_blocks(W) <= NW, "one owned (part) block per worker thread");
     constexpr int LPT = ((BW > 1 ? BW - 1 : 0) * 36 + NW - 1) / NW;  // L entries per worker (w >= 2)
-    constexpr int RFT = (W * 36 + NW - 1) / NW;           // refill entries per worker
     const int nrows = g.nrows, nsteps = g.nsteps;
-    double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
-    band_lds<BW>(lds, ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
+    double *col, *piv, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
+    band_lds<BW>(lds, ring, col, piv, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
     const int R = ring;
     const int RK = R + 1;                         // S^-1 / z of step k+1 are written during step k
     __shared__ int s_fail;
@@ -1832,71 +1838,66 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     const bool crit = tid < 64;                   // wave 0
     const int wt = tid - 64;                      // worker thread index
     if (tid == 0) s_fail = 0;
-    // rows 0..BW: block (r, r-w), w <= r, to diagonal w's slot r mod C_w
-    for (int t = tid; t < W * W * 36; t += NT) {
-        const int r = t / (W * 36), rem = t % (W * 36), w = rem / 36;
-        if (w <= r)
-            win[(size_t)(bd_base(W, w) + r % bd_cap(W, w)) * 36 + rem % 36] =
-                (r < nrows) ? g.Bd[((size_t)r * W) * 36 + rem] : 0.0;
+    // ---- the (part) block this worker owns: slot p of diagonal w, rows oh/6 .. oh/6+UR-1
+    const bool own = !crit && wt < UPB * bd_blocks(W);
+    int ow = 0, op = 0;
+    if (own) {
+        const int b = wt / UPB;
+        while (bd_base(W, ow + 1) <= b) ++ow;
+        op = b - bd_base(W, ow);
     }
-    for (int t = tid; t < W * 6; t += NT) bwin[t] = (t / 6 < nrows) ? g.bs[t] : 0.0;
-    // ---- per-worker static assignment; slot counters start at step 0
-    int u_wi[UPT], u_wj[UPT], u_h[UPT], u_bt[UPT], u_ba[UPT];
-    BdPos u_pt[UPT], u_pa[UPT];
+    const int oC = bd_cap(W, ow), oh = (max(wt, 0) % UPB) * UE;
+    int oo = ((op - ow) % oC + oC) % oC;          // offset at step 0
+    double t[UE];
+    {   // rows 0..BW (the spare slot's row W arrives during step 0)
+        const int i = ow + oo;
+        const bool ld = own && oo != oC - 1 && i < nrows;
+        const double *src = g.Bd + ((size_t)(ld ? i : 0) * W + ow) * 36 + oh;
 #pragma unroll
-    for (int q = 0; q < UPT; ++q) {
-        const int u = wt + q * NW;
-        const bool ok = !crit && u < NU;
-        const int pr = 1 + (ok ? u / 2 : 0);
-        int wi = 1;
-        while ((wi * (wi + 1)) / 2 <= pr) ++wi;
-        const int wj = pr - (wi - 1) * wi / 2 + 1;
-        u_wi[q] = ok ? wi : 1 << 20;               // never <= wmax when invalid
-        u_wj[q] = wj;
-        u_h[q] = (u & 1) * 18;
-        u_bt[q] = bd_base(W, wi - wj);             // target (k+wi, k+wj): diagonal wi-wj, row k+wi
-        u_pt[q] = BdPos{wi % bd_cap(W, wi - wj), bd_cap(W, wi - wj)};
-        u_ba[q] = bd_base(W, wj);                  // A_jk = (k+wj, k): diagonal wj, row k+wj
-        u_pa[q] = BdPos{wj % bd_cap(W, wj), bd_cap(W, wj)};
+        for (int j = 0; j < UE; ++j) t[j] = ld ? src[j] : 0.0;
+        if (own) {
+            double *dst = nullptr;
+            if (ow >= 1 && oo == 0) dst = col + (size_t)ow * 36;   // column 0
+            else if (ow == 0 && oo <= 1) dst = piv + oo * 36;      // pivots (0,0), (1,1)
+            if (dst)
+#pragma unroll
+                for (int j = 0; j < UE; ++j) dst[oh + j] = t[j];
+        }
     }
-    int l_w[LPT > 0 ? LPT : 1], l_e[LPT > 0 ? LPT : 1], l_b[LPT > 0 ? LPT : 1];
-    BdPos l_p[LPT > 0 ? LPT : 1];
-#pragma unroll
-    for (int q = 0; q < LPT; ++q) {
-        const int t = wt + 36 + q * NW;
-        const bool ok = !crit && t < BW * 36;
-        const int w = ok ? 1 + t / 36 : 1;
-        l_w[q] = ok ? w : 1 << 20;
-        l_e[q] = t % 36;
-        l_b[q] = bd_base(W, w);                    // A_{k+w,k}: diagonal w, row k+w
-        l_p[q] = BdPos{w % bd_cap(W, w), bd_cap(W, w)};
-    }
-    int r_dst[RFT];                                // refill: row k+W, block w = t/36
-    BdPos r_p[RFT];
-#pragma unroll
-    for (int q = 0; q < RFT; ++q) {
-        const int t = min(max(wt, 0) + q * NW, W * 36 - 1), w = t / 36;
-        r_dst[q] = bd_base(W, w) * 36 + t % 36;
-        r_p[q] = BdPos{W % bd_cap(W, w), bd_cap(W, w)};
-    }
-    BdPos c_p0{1 % bd_cap(W, 0), bd_cap(W, 0)}, c_p1{1 % bd_cap(W, 1), bd_cap(W, 1)};  // row k+1, diag 0 / 1
-    constexpr int cb1 = bd_base(W, 1);
-    double pf[RFT], pfn[RFT];
-    double pfb = 0.0, pfbn = 0.0;
-    auto prefetch = [&](int row, double (&dst)[RFT], double &dstb) {
-        const int rr = min(row, nrows - 1);
-#pragma unroll
-        for (int q = 0; q < RFT; ++q) dst[q] = g.Bd[((size_t)rr * W) * 36 + min(max(wt, 0) + q * NW, W * 36 - 1)];
-        dstb = g.bs[(size_t)rr * 6 + min(max(wt, 0), 5)];
+    for (int t2 = tid; t2 < W * 6; t2 += NT) bwin[t2] = (t2 / 6 < nrows) ? g.bs[t2] : 0.0;
+    // Entering rows (W blocks + the right-hand side) come in by direct global->LDS loads
+    // (global_load_lds_dwordx4, no VGPR destination): row r to staging buffer r & 1, issued by the
+    // worker waves at the start of step r-W-1's second phase and retired before its last barrier;
+    // the diagonal-BW block goes into the pivot column during step r-W, the rest into the owners'
+    // registers at the top of step r-BW. No owner register and no spill reload waits on a global
+    // load. Past the band's end the last row is loaded again (never read: readers stop at wmax).
+    constexpr int RW = W * 36 + 6, NPC = RW / 2;  // doubles per staged row, 16-byte pieces
+    __shared__ __attribute__((aligned(16))) double stgb[2 * RW];
+    auto stage_row = [&](int row, int wv, int lnv) {  // wv: worker wave index (uniform)
+        const int p = wv * 64 + lnv;
+        if (wv * 64 < NPC && p < NPC) {
+            const int rr = min(row, nrows - 1);
+            const double *src = p < W * 18 ? g.Bd + (size_t)rr * W * 36 + 2 * p : g.bs + (size_t)rr * 6 + 2 * (p - W * 18);
+            // inline asm rather than the builtin: with the builtin the compiler waits for the load
+            // before every later ds_read of the window (it cannot tell the LDS objects apart);
+            // this load is retired by the explicit vmcnt(0) before the step's last barrier
+            const unsigned dst = __builtin_amdgcn_readfirstlane(
+                (unsigned)(size_t)(__attribute__((address_space(3))) double *)(stgb + (size_t)(row & 1) * RW + wv * 128));
+            unsigned keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(src), "s"(dst)
+                         : "memory");
+        }
     };
-    if (!crit) prefetch(W, pfn, pfbn);
+    if (!crit) stage_row(W, (tid >> 6) - 1, lane);
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(tid) < 64) __builtin_amdgcn_s_setprio(3);
     // S_0^{-1}, y_0, z_0
     if (crit) {
         bool fail = false;
         double M = 0.0;
-        if (lane < 36) M = win[lane];              // block (0, 0): diagonal 0, slot 0
+        if (lane < 36) M = piv[lane];
         else if (lane < 42) { M = bwin[lane - 36]; ys[lane - 36] = M; }
         const double I = gj_inverse6(M, lane, fail);
         if (lane < 36) { Kv[lane] = I; ringK[lane] = I; }
@@ -1913,35 +1914,56 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     // a zero pivot sets s_fail and the sweep runs on (inf/NaN blocks are never used: the
     // caller drops the solve); no per-step LDS read of the flag on the critical chain
     for (int k = 0; k < nsteps; ++k) {
+        // per-lane indices made opaque each step: everything derived from them is recomputed in
+        // the step (a few integer ops) instead of being hoisted out of the loop as dozens of
+        // loop-invariant registers that then spill to scratch (a scratch reload waits for every
+        // outstanding global load, the spare-slot loads included)
+        int wtl = wt, lnl = lane, owl = ow, ohl = oh, oCl = oC;
+        asm volatile("" : "+v"(wtl), "+v"(lnl), "+v"(owl), "+v"(ohl), "+v"(oCl));
         const int kb = k & 1;
         const int wmax = min(BW, nrows - 1 - k);
         const double *Kk = Kv + kb * 36;
         const double *yk = ys + kb * 6;
+        const double *colk = col + (size_t)kb * W * 36;
         auto slot = [&](int w) { const int x = sk + w; return x >= W ? x - W : x; };
-        if (!crit) {
+        if (!crit && k > 0) {
+            // row k+BW (last step's spare slot) from its staging buffer into the owners' registers
+            // (bw 1: its block (k+1, k+1) is also this step's next pivot); its right-hand side into
+            // its row slot. (Its diagonal-BW block, this step's pivot-column entry, was copied in
+            // the previous step: phase 1 reads it before any barrier of this step.)
+            const double *sr = stgb + (size_t)((k + BW) & 1) * RW;
+            if (own && oo == oCl - 2) {
+                const double2 *src = (const double2 *)(sr + owl * 36 + ohl);
+                double2 *D = (BW == 1 && owl == 0) ? (double2 *)(piv + (kb ^ 1) * 36 + ohl) : nullptr;
 #pragma unroll
-            for (int q = 0; q < RFT; ++q) pf[q] = pfn[q];
-            pfb = pfbn;
-            prefetch(k + 1 + W, pfn, pfbn);
+                for (int v = 0; v < UE / 2; ++v) {
+                    const double2 x = src[v];
+                    t[2 * v] = x.x;
+                    t[2 * v + 1] = x.y;
+                    if (D) D[v] = x;
+                }
+            }
+            if (wtl < 6) bwin[slot(BW) * 6 + wtl] = k + BW < nrows ? sr[W * 36 + wtl] : 0.0;
         }
         STAMP(0);
         // ---- phase 1: L_{k+w,k} = A_{k+w,k} S_k^{-1}   (w = 1 on wave 0, w >= 2 on the workers)
         if (crit) {
-            if (lane < 36 && wmax >= 1) {
-                const int c = lane % 6;
-                const double *Aik = win + (size_t)(cb1 + c_p1.p) * 36 + (lane / 6) * 6;
+            if (lnl < 36 && wmax >= 1) {
+                const int c = lnl % 6;
+                const double *Aik = colk + 36 + (lnl / 6) * 6;
                 double v = 0.0;
 #pragma unroll
                 for (int m = 0; m < 6; ++m) v = fma(Aik[m], Kk[m * 6 + c], v);
-                Lcol[36 + lane] = v;
-                ringL[((size_t)kR * BW + 0) * 36 + lane] = v;
+                Lcol[36 + lnl] = v;
+                ringL[((size_t)kR * BW + 0) * 36 + lnl] = v;
             }
         } else {
 #pragma unroll
             for (int q = 0; q < LPT; ++q) {
-                const int w = l_w[q], e = l_e[q];
-                if (w <= wmax) {
-                    const double *Aik = win + (size_t)(l_b[q] + l_p[q].p) * 36 + (e / 6) * 6;
+                const int t2 = wtl + 36 + q * NW;
+                const int w = 1 + t2 / 36, e = t2 % 36;
+                if (t2 < BW * 36 && w <= wmax) {
+                    const double *Aik = colk + (size_t)w * 36 + (e / 6) * 6;
                     const int c = e % 6;
                     double v = 0.0;
 #pragma unroll
@@ -1954,78 +1976,83 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         STAMP(1);
         lds_barrier();
         STAMP(2);
-        // ---- phase 2
+        // ---- phase 2 (the worker waves first put row k+W+1 in flight)
+        if (!crit) stage_row(k + W + 1, (tid >> 6) - 1, lnl);
         if (crit) {
             if (k + 1 < nrows) {
                 const int s1 = slot(1), k1b = kb ^ 1;
                 // lanes 0..35: S_{k+1} = A_{k+1,k+1} - L_{k+1,k} A_{k+1,k}ᵀ
                 // lanes 36..41: y_{k+1} = b_{k+1} - L_{k+1,k} y_k
                 double M = 0.0;
-                if (lane < 42) {
-                    const bool mat = lane < 36;
-                    const int r = mat ? lane / 6 : lane - 36, c = mat ? lane % 6 : 0;
+                if (lnl < 42) {
+                    const bool mat = lnl < 36;
+                    const int r = mat ? lnl / 6 : lnl - 36, c = mat ? lnl % 6 : 0;
                     double sacc = 0.0;
                     if constexpr (BW >= 1) {
                         const double *L1 = Lcol + 36 + r * 6;
-                        const double *A1 = mat ? win + (size_t)(cb1 + c_p1.p) * 36 + c * 6 : yk;
+                        const double *A1 = mat ? colk + 36 + c * 6 : yk;
 #pragma unroll
                         for (int m = 0; m < 6; ++m) sacc = fma(L1[m], A1[m], sacc);
                     }
-                    double *dst = mat ? win + (size_t)c_p0.p * 36 + lane : bwin + s1 * 6 + r;
+                    double *dst = mat ? piv + k1b * 36 + lnl : bwin + s1 * 6 + r;
                     M = *dst - sacc;
                     *dst = M;
                     if (!mat) ys[k1b * 6 + r] = M;
                 }
                 bool fail = false;
-                const double I = gj_inverse6(M, lane, fail);
-                if (lane < 36) { Kv[k1b * 36 + lane] = I; ringK[kRK * 36 + lane] = I; }
-                else if (lane < 42) ringZ[kRK * 6 + lane - 36] = I;
+                const double I = gj_inverse6(M, lnl, fail);
+                if (lnl < 36) { Kv[k1b * 36 + lnl] = I; ringK[kRK * 36 + lnl] = I; }
+                else if (lnl < 42) ringZ[kRK * 6 + lnl - 36] = I;
                 // the look-ahead inverse past the last eliminated row (a separator row) is not a pivot
-                if (fail && lane == 0 && k + 1 < nsteps) s_fail = 1;
+                if (fail && lnl == 0 && k + 1 < nsteps) s_fail = 1;
             }
         } else {
-            // trailing update A_ij -= L_ik A_jkᵀ for all pairs (wi >= wj >= 1) except (1,1), three
-            // target rows per unit (same fma order per entry as one entry at a time)
+            // trailing update of the owned (part) block (k+wi, k+wj), wi = w+o, wj = o:
+            // A_ij -= L_ik A_jkᵀ (same fma order per entry as one entry at a time); (1,1) is wave 0's
+            const int wi = owl + oo;
+            if (own && oo >= 1 && oo != oCl - 1 && wi <= wmax && !(owl == 0 && oo == 1)) {
+                const double2 *Li = (const double2 *)(Lcol + wi * 36 + ohl);
+                const double2 *Aj = (const double2 *)(colk + (size_t)oo * 36);
+                double l[UE];
 #pragma unroll
-            for (int q = 0; q < UPT; ++q) {
-                if (u_wi[q] <= wmax) {
-                    const double2 *Li = (const double2 *)(Lcol + u_wi[q] * 36 + u_h[q]);
-                    const double2 *Aj = (const double2 *)(win + (size_t)(u_ba[q] + u_pa[q].p) * 36);
-                    double2 *T = (double2 *)(win + (size_t)(u_bt[q] + u_pt[q].p) * 36 + u_h[q]);
-                    double l[18];
+                for (int v = 0; v < UE / 2; ++v) { const double2 x = Li[v]; l[2 * v] = x.x; l[2 * v + 1] = x.y; }
 #pragma unroll
-                    for (int v = 0; v < 9; ++v) { const double2 x = Li[v]; l[2 * v] = x.x; l[2 * v + 1] = x.y; }
+                for (int c = 0; c < 6; ++c) {  // column c of the target = row c of A_jk
+                    double a[6];
 #pragma unroll
-                    for (int c = 0; c < 6; c += 2) {  // target columns c, c+1: rows c, c+1 of A_jk
-                        double a[12];
+                    for (int v = 0; v < 3; ++v) { const double2 x = Aj[c * 3 + v]; a[2 * v] = x.x; a[2 * v + 1] = x.y; }
 #pragma unroll
-                        for (int v = 0; v < 6; ++v) { const double2 x = Aj[c * 3 + v]; a[2 * v] = x.x; a[2 * v + 1] = x.y; }
+                    for (int r = 0; r < UR; ++r) {
+                        double sacc = 0.0;
 #pragma unroll
-                        for (int r = 0; r < 3; ++r) {
-                            double2 t = T[r * 3 + c / 2];
-                            double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-                            for (int m = 0; m < 6; ++m) {
-                                s0 = fma(l[r * 6 + m], a[m], s0);
-                                s1 = fma(l[r * 6 + m], a[6 + m], s1);
-                            }
-                            t.x -= s0;
-                            t.y -= s1;
-                            T[r * 3 + c / 2] = t;
-                        }
+                        for (int m = 0; m < 6; ++m) sacc = fma(l[r * 6 + m], a[m], sacc);
+                        t[r * 6 + c] -= sacc;
                     }
                 }
+                // next step's pivot column (k+1+w, k+1) / the pivot block after next (k+2, k+2)
+                double *dst = (owl >= 1 && oo == 1) ? col + ((size_t)(kb ^ 1) * W + owl) * 36
+                            : (owl == 0 && oo == 2) ? piv + kb * 36 : nullptr;
+                if (dst) {
+                    double2 *D = (double2 *)(dst + ohl);
+#pragma unroll
+                    for (int v = 0; v < UE / 2; ++v) D[v] = make_double2(t[2 * v], t[2 * v + 1]);
+                }
+            }
+            // the next pivot column's diagonal-BW entry (k+W, k+1), from row k+W's staging buffer
+            if (wtl < 18) {
+                const double *cs = stgb + (size_t)((k + W) & 1) * RW + BW * 36;
+                ((double2 *)(col + ((size_t)(kb ^ 1) * W + BW) * 36))[wtl] = ((const double2 *)cs)[wtl];
             }
             STAMP(5);
             // b_i -= L_ik y_k for w >= 2 (last worker wave)
             {
-                const int t = NW - 1 - wt;  // 0.. on the last wave
-                if (t < (wmax - 1) * 6) {
-                    const int wi = 2 + t / 6, r = t % 6;
+                const int t2 = NW - 1 - wtl;  // 0.. on the last wave
+                if (t2 < (wmax - 1) * 6) {
+                    const int wr = 2 + t2 / 6, r = t2 % 6;
                     double sacc = 0.0;
 #pragma unroll
-                    for (int m = 0; m < 6; ++m) sacc = fma(Lcol[wi * 36 + r * 6 + m], yk[m], sacc);
-                    bwin[slot(wi) * 6 + r] -= sacc;
+                    for (int m = 0; m < 6; ++m) sacc = fma(Lcol[wr * 36 + r * 6 + m], yk[m], sacc);
+                    bwin[slot(wr) * 6 + r] -= sacc;
                 }
             }
             STAMP(6);
@@ -2033,24 +2060,19 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                 const int k0 = k - kR;
                 const int cnt = kR + 1;
                 if constexpr (BW >= 1)
-                    for (int t = wt; t < cnt * BW * 36; t += NW) {
-                        const int st = t / (BW * 36), rem = t % (BW * 36), w = 1 + rem / 36, e = rem % 36;
+                    for (int t2 = wtl; t2 < cnt * BW * 36; t2 += NW) {
+                        const int st = t2 / (BW * 36), rem = t2 % (BW * 36), w = 1 + rem / 36, e = rem % 36;
                         const int i = k0 + st + w;
                         if (i < nrows) g.Lband[((size_t)i * W + w) * 36 + e] = ringL[(size_t)st * BW * 36 + rem];
                     }
-                for (int t = wt; t < cnt * 36; t += NW)
-                    g.Kinv[(size_t)k0 * 36 + t] = ringK[((k0 + t / 36) % RK) * 36 + t % 36];
-                for (int t = wt; t < cnt * 6; t += NW) g.zb[(size_t)k0 * 6 + t] = ringZ[((k0 + t / 6) % RK) * 6 + t % 6];
+                for (int t2 = wtl; t2 < cnt * 36; t2 += NW)
+                    g.Kinv[(size_t)k0 * 36 + t2] = ringK[((k0 + t2 / 36) % RK) * 36 + t2 % 36];
+                for (int t2 = wtl; t2 < cnt * 6; t2 += NW) g.zb[(size_t)k0 * 6 + t2] = ringZ[((k0 + t2 / 6) % RK) * 6 + t2 % 6];
             }
             STAMP(7);
-            // block row k+W enters: diagonal w's spare slot (row k+w-1's, column k-1 eliminated)
-            const bool live = k + W < nrows;
-#pragma unroll
-            for (int q = 0; q < RFT; ++q) {
-                const int t = wt + q * NW;
-                if (t < W * 36) win[(size_t)r_p[q].p * 36 + r_dst[q]] = live ? pf[q] : 0.0;
-            }
-            if (wt < 6) bwin[sk * 6 + wt] = live ? pfb : 0.0;
+            // the staged row lands before the barrier (issued at the start of this phase; read at
+            // the top of step k+2)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         STAMP(3);
         lds_barrier();
@@ -2058,14 +2080,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         sk = (sk + 1 == W) ? 0 : sk + 1;
         kR = (kR + 1 == R) ? 0 : kR + 1;
         kRK = (kRK + 1 == RK) ? 0 : kRK + 1;
-        c_p0.step();
-        c_p1.step();
-#pragma unroll
-        for (int q = 0; q < UPT; ++q) { u_pt[q].step(); u_pa[q].step(); }
-#pragma unroll
-        for (int q = 0; q < LPT; ++q) l_p[q].step();
-#pragma unroll
-        for (int q = 0; q < RFT; ++q) r_p[q].step();
+        oo = (oo == 0) ? oCl - 1 : oo - 1;
     }
 #ifdef PLBA_STAMPS
     if (stamps && (tid & 63) == 0)
@@ -2073,12 +2088,15 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
 #endif
     __syncthreads();  // drains every wave's flush stores: the backward pass reads them
     const bool failed = s_fail != 0;
-    if (g.sep && !failed) {  // rows nsteps..nsteps+BW-1 (all W blocks; eliminated columns as 0) and their right-hand sides
-        for (int t = tid; t < BW * W * 36; t += NT) {
-            const int i = t / (W * 36), rem = t % (W * 36), w = rem / 36, r = nsteps + i;
-            g.sep[t] = w <= i ? win[(size_t)(bd_base(W, w) + r % bd_cap(W, w)) * 36 + rem % 36] : 0.0;
+    if (g.sep && !failed) {  // rows nsteps..nsteps+BW-1, blocks w <= row (later columns) and their right-hand sides
+        const int i = ow + oo;  // separator row of the owned block (k = nsteps)
+        if (own && oo <= BW - ow && i < BW) {
+            double *dst = g.sep + ((size_t)i * W + ow) * 36 + oh;
+            const double *pv = piv + (nsteps & 1) * 36 + oh;  // (nsteps, nsteps) carries wave 0's last update
+#pragma unroll
+            for (int j = 0; j < UE; ++j) dst[j] = (ow == 0 && oo == 0) ? pv[j] : t[j];
         }
-        for (int t = tid; t < BW * 6; t += NT) g.sep[(size_t)BW * W * 36 + t] = bwin[((sk + t / 6) % W) * 6 + t % 6];
+        for (int t2 = tid; t2 < BW * 6; t2 += NT) g.sep[(size_t)BW * W * 36 + t2] = bwin[((sk + t2 / 6) % W) * 6 + t2 % 6];
     }
     return failed;
 }
@@ -2231,8 +2249,8 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d0) {
     const bool fail = band_forward<BW>(g, lds, d.ring, d.stamps) || diag_fail(d);
     if (threadIdx.x == 0) *d.solve_okp = fail ? 0 : 1;
     if (!fail && threadIdx.x < 64) {
-        double *win, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
-        band_lds<BW>(lds, d.ring, win, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
+        double *col, *piv, *bwin, *Lcol, *Kv, *xr, *part, *ys, *ringL, *ringK, *ringZ;
+        band_lds<BW>(lds, d.ring, col, piv, bwin, Lcol, Kv, xr, part, ys, ringL, ringK, ringZ);
         if constexpr (BW >= 1 && BW * 6 <= 64) band_backward_rl<BW>(d.Lband, d.zb, d.nf, d.nf, nullptr, d.xp, false, d.nf, threadIdx.x);
         else band_backward<BW>(d.Lband, d.zb, d.nf, d.nf, nullptr, d.xp, false, d.nf, xr, part, threadIdx.x);
     }
@@ -2245,11 +2263,11 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d0) {
 // block-reversed matrix Bd2), concurrently on two CUs. The two eliminated sets do not couple
 // (they are > BW blocks apart), so their Schur updates of the BW-block separator m..m+BW-1
 // add: S_sep = W0 + W1 − A_sep. The workgroup that finishes second solves the separator
-// (dense Gauss–Jordan, no pivoting: the pivots are LDLᵀ pivots, a zero one fails the solve as
+// (block LDLᵀ on its packed lower triangle, no pivoting: a zero pivot fails the solve as
 // SimplicialLDLT does) and runs both back substitutions on two waves. Half the serial chain.
 template <int BW>
 __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
-    constexpr int W = BW + 1, NT = kBandNT, NS = 6 * BW, LD = NS + 1;
+    constexpr int W = BW + 1, NT = kBandNT, NS = 6 * BW;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_last, s_sfail;
     const int seg = blockIdx.x, tid = threadIdx.x;
@@ -2295,14 +2313,18 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
     if (!s_sfail) {
     // merge layout (twisted_merge_doubles) from LDS offset 0: the band windows are dead, both
     // separators having been exported to global memory before the arrival
-    double *Ms = lds, *fcol = Ms + (size_t)NS * LD;
-    double *xr = fcol + 72 * BW, *part = xr + W * 6, *xr1 = part + W * 6, *part1 = xr1 + W * 6;
+    constexpr int NP = NS * (NS + 1) / 2;
+    double *Mp = lds;                                  // [NP] packed lower triangle, scalar rows
+    double *rhs = Mp + NP, *xs0 = rhs + NS, *xsr = xs0 + NS;  // [NS] each
+    double *Kp = xsr + NS, *Fb = Kp + (size_t)BW * 36;  // [BW][36] pivot inverses, [BW][36] L column
+    double *xr = Fb + (size_t)BW * 36, *part = xr + W * 6, *xr1 = part + W * 6, *part1 = xr1 + W * 6;
     double *xl = lds + twisted_merge_doubles(BW);  // [nf][6] x_p staging
+    auto mp = [&](int r, int c) -> double & { return Mp[r * (r + 1) / 2 + c]; };  // r >= c
     // ---- separator system S_sep (lower block (i,j), i >= j, w = i-j) and its right-hand side
     const double *W0 = d.tw_sep, *W1 = d.tw_sep + sep_stride;
     for (int t = tid; t < NS * NS; t += NT) {
-        const int R_ = t / NS, C_ = t % NS;
-        const int hi = R_ >= C_ ? R_ : C_, lo = R_ >= C_ ? C_ : R_;   // lower-triangle entry (hi, lo)
+        const int hi = t / NS, lo = t % NS;
+        if (lo > hi) continue;
         const int i = hi / 6, a = hi % 6, j = lo / 6, b = lo % 6, w = i - j;
         double v;
         if (w > BW) v = 0.0;
@@ -2312,67 +2334,81 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
             const double a0 = d.Bd[((size_t)(m + i) * W + w) * 36 + a * 6 + b];
             v = w0 + w1 - a0;
         }
-        Ms[(size_t)R_ * LD + C_] = v;
+        mp(hi, lo) = v;
     }
     for (int t = tid; t < NS; t += NT) {
         const int i = t / 6, a = t % 6;
-        Ms[(size_t)t * LD + NS] = W0[(size_t)BW * W * 36 + i * 6 + a] + W1[(size_t)BW * W * 36 + (BW - 1 - i) * 6 + a] -
-                                  d.bs[(size_t)(m + i) * 6 + a];
+        rhs[t] = W0[(size_t)BW * W * 36 + i * 6 + a] + W1[(size_t)BW * W * 36 + (BW - 1 - i) * 6 + a] -
+                 d.bs[(size_t)(m + i) * 6 + a];
     }
     if (tid == 0) s_sfail = 0;
     __syncthreads();
-    // block Gauss–Jordan with 6x6 pivots: wave 0 inverts the pivot block (its scalar pivots are
-    // the LDLᵀ pivots), then every other block row is eliminated in one parallel pass
-    double *Kp = fcol, *Fb = Kp + (size_t)BW * 36;  // [BW][36] pivot inverses, [BW][36] factors
+    // block LDLᵀ with 6x6 pivots on the packed lower triangle (no pivoting: the pivots are LDLᵀ
+    // pivots, a zero one fails the solve as SimplicialLDLT does); wave 0 inverts the pivot block,
+    // L_IP = A_IP S_PP⁻¹ goes to Fb, every trailing block and the right-hand side are updated in
+    // one parallel pass, then L_IP replaces A_IP in the triangle for the back substitution
     for (int P = 0; P < BW; ++P) {
         if (tid < 64) {
             bool f = false;
-            const double M = tid < 36 ? Ms[(size_t)(P * 6 + tid / 6) * LD + P * 6 + tid % 6] : 0.0;
+            const int a = tid / 6, b = tid % 6;
+            const double M = tid < 36 ? (a >= b ? mp(P * 6 + a, P * 6 + b) : mp(P * 6 + b, P * 6 + a)) : 0.0;
             const double I = gj_inverse6(M, tid, f);
             if (tid < 36) Kp[P * 36 + tid] = I;
             if (f && tid == 0) s_sfail = 1;
         }
         __syncthreads();
         if (s_sfail) break;
-        for (int t = tid; t < BW * 36; t += NT) {  // F_I = A_IP · A_PP⁻¹
-            const int I = t / 36, e = t % 36, a_ = e / 6, b_ = e % 6;
-            if (I == P) continue;
+        for (int t = tid; t < (BW - 1 - P) * 36; t += NT) {  // L_IP = A_IP · S_PP⁻¹, I > P
+            const int I = P + 1 + t / 36, e = t % 36, a_ = e / 6, b_ = e % 6;
             double acc = 0.0;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) acc = fma(Ms[(size_t)(I * 6 + a_) * LD + P * 6 + q], Kp[P * 36 + q * 6 + b_], acc);
-            Fb[t] = acc;
+            for (int q = 0; q < 6; ++q) acc = fma(mp(I * 6 + a_, P * 6 + q), Kp[P * 36 + q * 6 + b_], acc);
+            Fb[(I - P - 1) * 36 + e] = acc;
         }
         __syncthreads();
-        const int ncol = LD - P * 6;
-        for (int t = tid; t < NS * ncol; t += NT) {  // A_Ij -= F_I · A_Pj  (j >= pivot columns)
-            const int row = t / ncol, j = P * 6 + t % ncol, I = row / 6, a_ = row % 6;
-            if (I == P) continue;
-            double acc = 0.0;
+        const int nr = NS - (P + 1) * 6;  // trailing rows / columns
+        for (int t = tid; t < nr * (nr + 1); t += NT) {
+            const int rr = t / (nr + 1), cc = t % (nr + 1);
+            const int R_ = (P + 1) * 6 + rr;
+            if (cc == nr) {  // right-hand side: y_R -= L_R,P · y_P
+                double acc = 0.0;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) acc = fma(Fb[I * 36 + a_ * 6 + q], Ms[(size_t)(P * 6 + q) * LD + j], acc);
-            Ms[(size_t)row * LD + j] -= acc;
+                for (int q = 0; q < 6; ++q) acc = fma(Fb[(R_ / 6 - P - 1) * 36 + (R_ % 6) * 6 + q], rhs[P * 6 + q], acc);
+                rhs[R_] -= acc;
+                continue;
+            }
+            const int C_ = (P + 1) * 6 + cc;
+            if (C_ > R_) continue;
+            double acc = 0.0;  // A_RC -= L_R,P · A_C,Pᵀ
+#pragma unroll
+            for (int q = 0; q < 6; ++q) acc = fma(Fb[(R_ / 6 - P - 1) * 36 + (R_ % 6) * 6 + q], mp(C_, P * 6 + q), acc);
+            mp(R_, C_) -= acc;
+        }
+        __syncthreads();
+        for (int t = tid; t < (BW - 1 - P) * 36; t += NT) {
+            const int I = P + 1 + t / 36, e = t % 36;
+            mp(I * 6 + e / 6, P * 6 + e % 6) = Fb[(I - P - 1) * 36 + e];
         }
         __syncthreads();
     }
-    __syncthreads();
 #ifdef PLBA_STAMPS
     unsigned long long tw_t2 = __builtin_readcyclecounter();
     TW_MARK(2, tw_t2 - tw_t1);
 #endif
     if (!s_sfail) {
-    // x_sep in both segment orders (fcol is free now): rows m+i for segment 0, reversed rows
-    // n1+i = original m+BW-1-i for segment 1
-    double *xs0 = Fb;  // factors are free now
-    for (int t = tid; t < NS; t += NT) {  // x_P = A_PP⁻¹ rhs_P (block rows are decoupled now)
-        const int P = t / 6, a_ = t % 6;
-        double x = 0.0;
+    // back substitution x_P = S_PP⁻¹ y_P − Σ_{I>P} L_IPᵀ x_I; x_sep in both segment orders: rows m+i
+    // for segment 0, reversed rows n1+i = original m+BW-1-i for segment 1
+    for (int P = BW - 1; P >= 0; --P) {
+        if (tid < 6) {
+            double x = 0.0;
 #pragma unroll
-        for (int q = 0; q < 6; ++q) x = fma(Kp[P * 36 + a_ * 6 + q], Ms[(size_t)(P * 6 + q) * LD + NS], x);
-        xs0[t] = x;
-        xl[(size_t)m * 6 + t] = x;
+            for (int q = 0; q < 6; ++q) x = fma(Kp[P * 36 + tid * 6 + q], rhs[P * 6 + q], x);
+            for (int R_ = (P + 1) * 6; R_ < NS; ++R_) x -= mp(R_, P * 6 + tid) * xs0[R_];
+            xs0[P * 6 + tid] = x;
+            xl[(size_t)m * 6 + P * 6 + tid] = x;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    double *xsr = Ms;  // reversed-order copy (Ms is no longer needed)
     for (int t = tid; t < NS; t += NT) xsr[t] = xs0[(BW - 1 - t / 6) * 6 + t % 6];
     __syncthreads();
     if constexpr (BW * 6 <= 64) {

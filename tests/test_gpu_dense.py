@@ -91,14 +91,14 @@ def test_dense_mfma_factorisation(solver, monkeypatch, cfg, kw):
 
 
 def test_revisit_window_wide_band(solver):
-    """C3R: the loop revisit folds (RCM) into a band of 23 pose blocks — wider than the 20 a
-    row-slot LDS window holds — so it runs the diagonal-ring window of k_rcs_factor_band
-    (bw 21..28) instead of the dense path; parity with the oracle."""
+    """C3R: the loop revisit folds (RCM) into a band of 23 pose blocks — wider than the 20 the
+    former LDS window held — so it runs k_rcs_factor_band's register-resident window (bw up to
+    kBandMax = 24) instead of the dense path; parity with the oracle."""
     g = synth.generate("C3R")
     ref = oa.lba_plucker(g)
     solver.upload(g)
     st = solver.structure_stats()
-    assert st["banded"] == 1 and 20 < st["bw"] <= 28 and st["dense_mfma"] == 0, st
+    assert st["banded"] == 1 and 20 < st["bw"] <= 24 and st["dense_mfma"] == 0, st
     _check(solver.lba_plucker(), ref)
 
 

@@ -139,10 +139,10 @@ def test_speculative_slots_on_block_cyclic_reduction_are_bitwise(cfg):
 
 
 @pytest.mark.parametrize("cfg,kw", [("C2R", {}), ("C1", dict(n_kf=30, n_pt=400, seed=35, track_max=30))])
-def test_speculative_slots_on_the_lds_window_band_kernel_are_bitwise(cfg, kw):
-    """Trial slots on the LDS-window band kernels (grid.y = slot; per-slot band, factors and
-    separator windows): C2R runs the two-sided kernel at bw 20, the 30-KF window the one-sided
-    diagonal-ring window at bw 26. Bitwise the one-slot solve, with forced solve failures too."""
+def test_speculative_slots_on_the_band_window_kernels_are_bitwise(cfg, kw):
+    """Trial slots on the band kernels with the register-resident window (grid.y = slot; per-slot
+    band, factors and separator windows): C2R runs the two-sided kernel at bw 20, the 30-KF window
+    the one-sided kernel at bw 21. Bitwise the one-slot solve, with forced solve failures too."""
     g = synth.generate(cfg, **kw)
     for diag in (0, 128):
         base, base2, st0 = _solve(g, 1, 0, diag=diag)
