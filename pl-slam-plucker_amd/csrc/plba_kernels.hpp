@@ -1808,11 +1808,11 @@ __host__ __device__ constexpr size_t band_lds_doubles(int bw, int R) {
     return (size_t)(bw + 1) * 72 + 72 + (size_t)(bw + 1) * (6 + 36 + 6 + 6) + 72 + 12 + (size_t)R * bw * 36 +
            (size_t)(R + 1) * 42;
 }
-// static LDS of band_forward: the entering rows' staging buffers [3][W*36 + 6] (blocks, right-hand
+// static LDS of band_forward: the entering rows' staging buffers [2][W*36 + 6] (blocks, right-hand
 // side) plus a few flags. A separate LDS object from the dynamic window, so that the compiler can
 // tell the direct global->LDS loads into it from the window's reads (with one LDS object every
 // ds_read after such a load waits for it)
-__host__ __device__ constexpr size_t band_static_bytes(int bw) { return 24 * ((size_t)(bw + 1) * 36 + 6) + 64; }
+__host__ __device__ constexpr size_t band_static_bytes(int bw) { return 16 * ((size_t)(bw + 1) * 36 + 6) + 64; }
 // The twisted kernel's merge, after both segments have exported their separator windows, reuses
 // the LDS from 0: the separator system's packed lower triangle [6bw(6bw+1)/2], its right-hand side
 // and two solution copies [3][6bw], pivot inverses + one L column [2][bw][36], two backward rings
@@ -1866,13 +1866,13 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     }
     for (int t2 = tid; t2 < W * 6; t2 += NT) bwin[t2] = (t2 / 6 < nrows) ? g.bs[t2] : 0.0;
     // Entering rows (W blocks + the right-hand side) come in by direct global->LDS loads
-    // (global_load_lds_dwordx4, no VGPR destination): row r to staging buffer r % 3, issued by the
-    // worker waves at the top of step r-W-1 and retired before that step's first barrier; the
-    // diagonal-BW block goes into the pivot column during step r-W, the rest into the owners'
-    // registers at the top of step r-BW. No owner register and no spill reload of the update phase
-    // waits on a global load. Past the band's end the last row is loaded again (never read).
+    // (global_load_lds_dwordx4, no VGPR destination): row r to staging buffer r & 1, issued by the
+    // worker waves at the start of step r-W-1's second phase and retired before its last barrier;
+    // the diagonal-BW block goes into the pivot column during step r-W, the rest into the owners'
+    // registers at the top of step r-BW. No owner register and no spill reload waits on a global
+    // load. Past the band's end the last row is loaded again (never read: readers stop at wmax).
     constexpr int RW = W * 36 + 6, NPC = RW / 2;  // doubles per staged row, 16-byte pieces
-    __shared__ __attribute__((aligned(16))) double stgb[3 * RW];
+    __shared__ __attribute__((aligned(16))) double stgb[2 * RW];
     auto stage_row = [&](int row, int wv, int lnv) {  // wv: worker wave index (uniform)
         const int p = wv * 64 + lnv;
         if (wv * 64 < NPC && p < NPC) {
@@ -1882,7 +1882,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
             // before every later ds_read of the window (it cannot tell the LDS objects apart);
             // this load is retired by the explicit vmcnt(0) before the step's last barrier
             const unsigned dst = __builtin_amdgcn_readfirstlane(
-                (unsigned)(size_t)(__attribute__((address_space(3))) double *)(stgb + (size_t)(row % 3) * RW + wv * 128));
+                (unsigned)(size_t)(__attribute__((address_space(3))) double *)(stgb + (size_t)(row & 1) * RW + wv * 128));
             unsigned keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                          : "=&s"(keep)
@@ -1891,7 +1891,6 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         }
     };
     if (!crit) stage_row(W, (tid >> 6) - 1, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(tid) < 64) __builtin_amdgcn_s_setprio(3);
     // S_0^{-1}, y_0, z_0
@@ -1932,25 +1931,20 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
             // (bw 1: its block (k+1, k+1) is also this step's next pivot); its right-hand side into
             // its row slot. (Its diagonal-BW block, this step's pivot-column entry, was copied in
             // the previous step: phase 1 reads it before any barrier of this step.)
-            const double *sr = stgb + (size_t)((k + BW) % 3) * RW;
-            {   // every worker reads (a valid address) and selects: the owned registers keep one
-                // assignment per step instead of a branch-local copy the compiler shuffles and spills
-                const bool cp = own && oo == oCl - 2;
+            const double *sr = stgb + (size_t)((k + BW) & 1) * RW;
+            if (own && oo == oCl - 2) {
                 const double2 *src = (const double2 *)(sr + owl * 36 + ohl);
-                double2 *D = (cp && BW == 1 && owl == 0) ? (double2 *)(piv + (kb ^ 1) * 36 + ohl) : nullptr;
+                double2 *D = (BW == 1 && owl == 0) ? (double2 *)(piv + (kb ^ 1) * 36 + ohl) : nullptr;
 #pragma unroll
                 for (int v = 0; v < UE / 2; ++v) {
                     const double2 x = src[v];
-                    t[2 * v] = cp ? x.x : t[2 * v];
-                    t[2 * v + 1] = cp ? x.y : t[2 * v + 1];
+                    t[2 * v] = x.x;
+                    t[2 * v + 1] = x.y;
                     if (D) D[v] = x;
                 }
             }
             if (wtl < 6) bwin[slot(BW) * 6 + wtl] = k + BW < nrows ? sr[W * 36 + wtl] : 0.0;
         }
-        // row k+W+1 in flight during phase 1 (third buffer: this step reads rows k+BW and k+W);
-        // retired before the barrier that ends phase 1, so no spill reload of phase 2 waits on it
-        if (!crit) stage_row(k + W + 1, (tid >> 6) - 1, lnl);
         STAMP(0);
         // ---- phase 1: L_{k+w,k} = A_{k+w,k} S_k^{-1}   (w = 1 on wave 0, w >= 2 on the workers)
         if (crit) {
@@ -1979,11 +1973,11 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                 }
             }
         }
-        if (!crit) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP(1);
         lds_barrier();
         STAMP(2);
-        // ---- phase 2
+        // ---- phase 2 (the worker waves first put row k+W+1 in flight)
+        if (!crit) stage_row(k + W + 1, (tid >> 6) - 1, lnl);
         if (crit) {
             if (k + 1 < nrows) {
                 const int s1 = slot(1), k1b = kb ^ 1;
@@ -2046,7 +2040,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
             }
             // the next pivot column's diagonal-BW entry (k+W, k+1), from row k+W's staging buffer
             if (wtl < 18) {
-                const double *cs = stgb + (size_t)((k + W) % 3) * RW + BW * 36;
+                const double *cs = stgb + (size_t)((k + W) & 1) * RW + BW * 36;
                 ((double2 *)(col + ((size_t)(kb ^ 1) * W + BW) * 36))[wtl] = ((const double2 *)cs)[wtl];
             }
             STAMP(5);
@@ -2076,6 +2070,9 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                 for (int t2 = wtl; t2 < cnt * 6; t2 += NW) g.zb[(size_t)k0 * 6 + t2] = ringZ[((k0 + t2 / 6) % RK) * 6 + t2 % 6];
             }
             STAMP(7);
+            // the staged row lands before the barrier (issued at the start of this phase; read at
+            // the top of step k+2)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         STAMP(3);
         lds_barrier();
