@@ -467,8 +467,8 @@ inline hipError_t launch_band(Dev &d, hipStream_t s) {
         return hipLaunchKernel(k, dim3(d.twisted ? 2 : 1, d.spec_max), dim3(kClNT), args, cl_lds_bytes(d.bw, d.nf, d.twisted != 0), s);
     }
     if (d.twisted)
-        return hipLaunchKernel(twisted_kernel(d.bw), dim3(2, d.spec_max), dim3(kBandNT), args, twisted_lds_bytes(d.bw, d.nf), s);
-    return hipLaunchKernel(band_kernel(d.bw), dim3(1, d.spec_max), dim3(kBandNT), args, band_lds_bytes(d.bw, d.nf), s);
+        return hipLaunchKernel(twisted_kernel(d.bw), dim3(2, d.spec_max), dim3(band_nt(d.bw)), args, twisted_lds_bytes(d.bw, d.nf), s);
+    return hipLaunchKernel(band_kernel(d.bw), dim3(1, d.spec_max), dim3(band_nt(d.bw)), args, band_lds_bytes(d.bw, d.nf), s);
 }
 
 // time a launch when kernel timing is enabled

@@ -44,14 +44,18 @@ constexpr int kLmBlock = 64;  // landmark-parallel kernels: 24k landmarks at C3 
 constexpr int kChunk = PLBA_CHUNK;  // Schur triples per assembly wave (4 per lane)
 constexpr int kTraceCap = 64;
 constexpr int kTile = 32;   // RCS factorisation tile (dense fallback)
-constexpr int kBandMax = 24; // widest envelope (in pose blocks) the register-window factorisation holds
+constexpr int kBandMax = 27; // widest envelope (in pose blocks) the register-window factorisation holds
 #ifndef PLBA_BAND_NT
 #define PLBA_BAND_NT 768
 #endif
-constexpr int kBandNT = PLBA_BAND_NT; // threads of the banded factorisation workgroup
+constexpr int kBandNT = PLBA_BAND_NT; // threads of the banded factorisation workgroup (bw <= 24)
 // rows of a band block one worker owns in registers (plba_kernels.hpp band_forward): whole 6x6
 // blocks at 512 threads (256 VGPRs), half blocks when more, smaller waves are configured
-constexpr int kBandUR = kBandNT <= 512 ? 6 : 3;
+// Bandwidths 25..27 need more owned blocks than 704 worker threads hold at three rows each: they
+// run 512-thread workgroups owning whole blocks (256 VGPRs, no scratch; at bw 23 that form was 6 %
+// slower than 768 threads at half blocks)
+__host__ __device__ constexpr int band_nt(int bw) { return bw <= 24 ? kBandNT : 512; }
+__host__ __device__ constexpr int band_ur(int bw) { return band_nt(bw) <= 512 ? 6 : 3; }
 // Speculative trials (DESIGN §2 "Speculative trials"): a step may evaluate up to kMaxSpec damped
 // trials of one linearisation at once — λ, λ·ν, λ·ν·2ν, ... (exactly the λ sequence g2o's
 // Levenberg loop walks after rejections) — in trial slots 0..W-1 (blockIdx.y of the trial
@@ -1772,15 +1776,16 @@ struct BandSeg {
 };
 
 // Register-resident band window. Block (i, i-w) of a live row is owned by a pair of worker
-// threads (3 rows each) for its whole life in the window and updated in registers; it is written
-// to LDS once, when it becomes part of the next pivot column (the step's operand A_jk and the
-// source of L), or, on the diagonal, when it becomes the next pivot block. Ownership follows
-// diagonal-major rings: diagonal w has C_w = W-w+1 slots, row i in slot i mod C_w; at step k
-// the slot's offset o = (slot - k - w) mod C_w says which row it holds (i = k+w+o): o = 0 the
-// pivot column, 1 <= o <= BW-w a trailing block (pair wi = w+o, wj = o), o = C_w-1 the spare slot
-// that loads the entering row k+W from global memory during step k. W(W+3) half blocks
-// (bw 23: 648 of the 960 worker threads); LDS keeps only two pivot columns, the pivot blocks and
-// the L / S^-1 / z staging rings, so no read-modify-write of the trailing blocks goes through LDS.
+// threads (3 rows each; whole blocks on one thread for bw 25..27) for its whole life in the
+// window and updated in registers; it is written to LDS once, when it becomes part of the next
+// pivot column (the step's operand A_jk and the source of L), or, on the diagonal, when it becomes
+// the next pivot block. Ownership follows diagonal-major rings: diagonal w has C_w = W-w+1 slots,
+// row i in slot i mod C_w; at step k the slot's offset o = (slot - k - w) mod C_w says which row
+// it holds (i = k+w+o): o = 0 the pivot column, 1 <= o <= BW-w a trailing block (pair wi = w+o,
+// wj = o), o = C_w-1 the spare slot whose row k+W enters (staged, below). W(W+3) half blocks
+// (bw 23: 648 of the 704 worker threads of a 768-thread workgroup); LDS keeps only two pivot
+// columns, the pivot blocks, the staged rows and the L / S^-1 / z staging rings, so no
+// read-modify-write of the trailing blocks goes through LDS.
 __host__ __device__ constexpr int bd_cap(int W, int w) { return W - w + 1; }
 __host__ __device__ constexpr int bd_base(int W, int w) { return w * (W + 1) - w * (w - 1) / 2; }
 __host__ __device__ constexpr int bd_blocks(int W) { return W * (W + 3) / 2; }
@@ -1823,8 +1828,8 @@ __host__ __device__ constexpr size_t twisted_merge_doubles(int bw) {
 
 template <int BW>
 __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int ring, unsigned long long *stamps) {
-    constexpr int NT = kBandNT, W = BW + 1, NW = NT - 64;
-    constexpr int UR = kBandUR, UPB = 6 / UR, UE = UR * 6;  // rows per owner, owners per block, entries
+    constexpr int NT = band_nt(BW), W = BW + 1, NW = NT - 64;
+    constexpr int UR = band_ur(BW), UPB = 6 / UR, UE = UR * 6;  // rows per owner, owners per block, entries
     static_assert(UPB * bd_blocks(W) <= NW, "one owned (part) block per worker thread");
     constexpr int LPT = ((BW > 1 ? BW - 1 : 0) * 36 + NW - 1) / NW;  // L entries per worker (w >= 2)
     const int nrows = g.nrows, nsteps = g.nsteps;
@@ -1874,21 +1879,23 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     constexpr int RW = W * 36 + 6, NPC = RW / 2;  // doubles per staged row, 16-byte pieces
     __shared__ __attribute__((aligned(16))) double stgb[2 * RW];
     auto stage_row = [&](int row, int wv, int lnv) {  // wv: worker wave index (uniform)
-        const int p = wv * 64 + lnv;
-        if (wv * 64 < NPC && p < NPC) {
+      for (int pb = wv * 64; pb < NPC; pb += NW) {  // (more pieces than worker lanes at bw >= 24)
+        const int p = pb + lnv;
+        if (p < NPC) {
             const int rr = min(row, nrows - 1);
             const double *src = p < W * 18 ? g.Bd + (size_t)rr * W * 36 + 2 * p : g.bs + (size_t)rr * 6 + 2 * (p - W * 18);
             // inline asm rather than the builtin: with the builtin the compiler waits for the load
             // before every later ds_read of the window (it cannot tell the LDS objects apart);
             // this load is retired by the explicit vmcnt(0) before the step's last barrier
             const unsigned dst = __builtin_amdgcn_readfirstlane(
-                (unsigned)(size_t)(__attribute__((address_space(3))) double *)(stgb + (size_t)(row & 1) * RW + wv * 128));
+                (unsigned)(size_t)(__attribute__((address_space(3))) double *)(stgb + (size_t)(row & 1) * RW + pb * 2));
             unsigned keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                          : "=&s"(keep)
                          : "v"(src), "s"(dst)
                          : "memory");
         }
+      }
     };
     if (!crit) stage_row(W, (tid >> 6) - 1, lane);
     __syncthreads();
@@ -2242,7 +2249,7 @@ __device__ __forceinline__ void band_backward(const double *Lband, const double 
 }
 
 template <int BW>
-__global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d0) {
+__global__ __launch_bounds__(band_nt(BW)) void k_rcs_factor_band(Dev d0) {
     TRIAL_SLOT(blockIdx.y)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const BandSeg g{d.Bd, d.bs, d.Lband, d.Kinv, d.zb, d.nf, d.nf, nullptr};
@@ -2255,7 +2262,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d0) {
         else band_backward<BW>(d.Lband, d.zb, d.nf, d.nf, nullptr, d.xp, false, d.nf, xr, part, threadIdx.x);
     }
     __syncthreads();
-    pose_update_wg<kBandNT>(d, fail);  // applied even after a failed solve, with the previous x_p (A13)
+    pose_update_wg<band_nt(BW)>(d, fail);  // applied even after a failed solve, with the previous x_p (A13)
 }
 
 // Two-sided ("twisted") banded LDLᵀ: workgroup 0 eliminates block rows 0..m-1 top-down,
@@ -2267,7 +2274,7 @@ __global__ __launch_bounds__(kBandNT) void k_rcs_factor_band(Dev d0) {
 // SimplicialLDLT does) and runs both back substitutions on two waves. Half the serial chain.
 template <int BW>
 __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
-    constexpr int W = BW + 1, NT = kBandNT, NS = 6 * BW;
+    constexpr int W = BW + 1, NT = band_nt(BW), NS = 6 * BW;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ int s_last, s_sfail;
     const int seg = blockIdx.x, tid = threadIdx.x;
@@ -2433,7 +2440,7 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
 }
 
 template <int BW>
-__global__ __launch_bounds__(kBandNT) void k_rcs_factor_twisted(Dev d0) {
+__global__ __launch_bounds__(band_nt(BW)) void k_rcs_factor_twisted(Dev d0) {
     if constexpr (BW >= 1) {  // (the host never selects bw 0)
         TRIAL_SLOT(blockIdx.y)
         k_rcs_factor_twisted_body<BW>(d);

@@ -93,12 +93,49 @@ def test_dense_mfma_factorisation(solver, monkeypatch, cfg, kw):
 def test_revisit_window_wide_band(solver):
     """C3R: the loop revisit folds (RCM) into a band of 23 pose blocks — wider than the 20 the
     former LDS window held — so it runs k_rcs_factor_band's register-resident window (bw up to
-    kBandMax = 24) instead of the dense path; parity with the oracle."""
+    kBandMax = 27) instead of the dense path; parity with the oracle."""
     g = synth.generate("C3R")
     ref = oa.lba_plucker(g)
     solver.upload(g)
     st = solver.structure_stats()
     assert st["banded"] == 1 and 20 < st["bw"] <= 24 and st["dense_mfma"] == 0, st
+    _check(solver.lba_plucker(), ref)
+
+
+def _ids_in_order(g, order):
+    """Keyframe ids that put the free poses in `order` (the id order g2o builds the Hessian in);
+    fixed keyframes after them."""
+    h = g.copy()
+    free = np.where(g.kf_fixed == 0)[0]
+    fixed = np.where(g.kf_fixed != 0)[0]
+    ids = np.empty(g.n_kf, np.int32)
+    ids[free[order]] = np.arange(len(free), dtype=np.int32)
+    ids[fixed] = len(free) + np.arange(len(fixed), dtype=np.int32)
+    h.kf_id = ids
+    return h
+
+
+def test_band_window_at_the_widest_band(solver, monkeypatch):
+    """Bandwidths 25..kBandMax = 27 run 512-thread band workgroups owning whole 6x6 blocks (bw <= 24:
+    768 threads, half blocks). C3R in SciPy's reverse Cuthill-McKee order (bandwidth 27; this
+    library's own RCM finds 23) with the reordering off: banded at bw 27, parity with the oracle."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    g = synth.generate("C3R")
+    free = np.where(g.kf_fixed == 0)[0]
+    hid = -np.ones(g.n_kf, np.int64)
+    hid[free] = np.arange(len(free))
+    lm = np.concatenate([g.ept_lm, g.n_pt + g.eln_lm])
+    kf = np.concatenate([g.ept_kf, g.eln_kf])
+    m = hid[kf] >= 0
+    A = sp.csr_matrix((np.ones(int(m.sum())), (hid[kf[m]], lm[m])), shape=(len(free), g.n_pt + g.n_ln))
+    order = np.asarray(reverse_cuthill_mckee((A @ A.T).tocsr(), symmetric_mode=True))
+    h = _ids_in_order(g, order)
+    monkeypatch.setenv("PLBA_NO_RCM", "1")
+    ref = oa.lba_plucker(h)
+    solver.upload(h)
+    st = solver.structure_stats()
+    assert st["banded"] == 1 and 24 < st["bw"] <= 27 and st["dense_mfma"] == 0, st
     _check(solver.lba_plucker(), ref)
 
 
