@@ -164,3 +164,19 @@ def test_gba_c5_bounded_matches_oracle_fixture(solver):
     close(out["kf_Tcw"], ref["kf_Tcw"], ref["init_kf_Tcw"], "kf_Tcw")
     close(np.asarray(out["pt_xyz"]).reshape(-1, 3)[ref["pt_idx"]], ref["pt_xyz"], ref["init_pt"], "pt_xyz")
     close(np.asarray(out["ln_line3d"]).reshape(-1, 6)[ref["ln_idx"]], ref["ln_line3d"], ref["init_ln"], "ln_line3d")
+
+
+@pytest.mark.parametrize("gba", [False, True], ids=["hlm", "gba"])
+def test_hlm_through_the_wide_band_kernel(solver, gba):
+    """The hand-rolled LM and GBA step graphs (Ctrl::hlm 1 / 2) on a window whose reduced camera
+    system is a band of ~20 pose blocks: the register-window band kernel (bw 10..27) factorises it
+    and applies their pose update, as the column-lane and BCR kernels do for the other tests."""
+    from plba.hlm import gba_window
+    g = synth.generate("C1", n_kf=30, n_pt=400, seed=35, track_min=2, track_max=30, fixed_frac=0.1)
+    win = gba_window(g) if gba else hlm_window(g)
+    p = capi.gba_params() if gba else capi.hlm_params()
+    ref = oa.hlm_lba(win, p)
+    solver.upload(win.graph)
+    st = solver.structure_stats()
+    assert st["banded"] == 1 and st["column_lane"] == 0 and st["bcr_rows"] == 0 and st["bw"] >= 10, st
+    _compare(solver.hlm_lba(win, p), ref, win)
