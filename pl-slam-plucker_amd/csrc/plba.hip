@@ -441,8 +441,10 @@ inline SpecChoice spec_choice(bool band1, bool wide, bool bcr, int bcr_fit, bool
         cap = std::min(cap, bcr_fit);
     }
     // wide bands (bw > 9: the register-window kernel, ≈0.5 ms a factorisation at C3R) take every
-    // slot: C3R 21 -> 17 steps per LBA, 1,000 -> 1,194 LM it/s (2 / 3 / 4 slots)
-    r.slots = wide ? kMaxSpec : 2;
+    // slot: C3R 21 -> 17 steps per LBA, 1,000 -> 1,194 LM it/s (2 / 3 / 4 slots); so do
+    // BCR windows, as far as the device holds the slots' super-rows (C4: 4 fit, 22 -> 17 steps,
+    // 1,822 -> 1,851 LM it/s); the column-lane windows keep two (C3: 3 slots 5,248 vs 5,304)
+    r.slots = (wide || bcr) ? kMaxSpec : 2;
     r.policy = kSpecSticky;
     const char *e = getenv("PLBA_SPEC");
     if (e && e[0]) r.slots = std::max(1, std::min(atoi(e), kMaxSpec));

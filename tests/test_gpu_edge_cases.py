@@ -95,9 +95,10 @@ def test_shuffled_edges_and_ids(solver):
     assert np.abs(out["pt_xyz"] - base["pt_xyz"][pp]).max() < 1e-8
 
 
-@pytest.mark.parametrize("tmax,n_kf,banded", [(12, 24, 1), (30, 30, 1), (60, 60, 0)])
+@pytest.mark.parametrize("tmax,n_kf,banded", [(12, 24, 1), (12, 12, 1), (16, 16, 1), (30, 30, 1), (60, 60, 0)])
 def test_wide_bands_and_dense_fallback(solver, monkeypatch, tmax, n_kf, banded):
-    # tmax 12 -> banded kernel with bw 11; tmax 30 -> bw 21 (register-resident band window, up
+    # tmax 12 -> banded kernel with bw 11; 12 / 16 KF -> the band spans every free pose (bw = nf-1:
+    # the register window starts full and no row ever enters); tmax 30 -> bw 21 (register-resident band window, up
     # to kBandMax = 27); the 60-KF window with scrambled keyframe ids and no reordering -> an
     # envelope wider than kBandMax (dense path)
     g = synth.generate("C1", n_kf=n_kf, n_pt=400, seed=5 + tmax, track_min=2, track_max=tmax, fixed_frac=0.1)
