@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d0) {
     if (xcd >= full && slot >= per - 1) return;  // padding
     const int ch = xcd < full ? xcd * per + slot : full * per + (xcd - full) * (per - 1) + slot;
     const int lane = threadIdx.x;
-    const bool hlm = d.ctrl->hlm != 0;
+    const int hlm = d.ctrl->hlm;
     const int b = d.ch_blk[ch];
     const bool diag = d.blk_i1[b] == d.blk_i2[b];
     double acc[42];
@@ -1176,7 +1176,8 @@ __global__ __launch_bounds__(64) void k_rcs_chunk(Dev d0) {
             }
             // hand-rolled LM: A has one live row, so only m00 is used — and a GBA line's Z_e
             // (6 entries) spills into Z's second row: the full 8-entry product
-            if (hlm) m00 += m11;
+            if (hlm == 1) m00 = m01;  // z_1 · (S z_2): row 1 of Z carries S z_0 (edge_schur_body)
+            else if (hlm) m00 += m11;
             double Q[12];
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
@@ -1240,7 +1241,7 @@ __global__ __launch_bounds__(64, PLBA_CHH_MINB) void k_rcs_chunk_h(Dev d0) {
     if (xcd >= full && slot >= per - 1) return;  // padding
     const int ch = xcd < full ? xcd * per + slot : full * per + (xcd - full) * (per - 1) + slot;
     const int lane = threadIdx.x, p = lane & (NB - 1), h = lane >> 5;
-    const bool hlm = d.ctrl->hlm != 0;
+    const int hlm = d.ctrl->hlm;
     const int b = d.ch_blk[ch];
     const bool diag = d.blk_i1[b] == d.blk_i2[b];
     double acc[21];
@@ -1303,7 +1304,8 @@ __global__ __launch_bounds__(64, PLBA_CHH_MINB) void k_rcs_chunk_h(Dev d0) {
                 m11 = fma(z1[4 + k], z2[4 + k], m11);
             }
         }
-        if (hlm) m00 += m11;  // (as k_rcs_chunk)
+        if (hlm == 1) m00 = m01;  // (as k_rcs_chunk)
+        else if (hlm) m00 += m11;
         // Q = (Z₁Z₂ᵀ) A₂ from the A₂ row (read rotated as k_rcs_chunk), then this lane's A₁
         // entries 3h .. 3h+2 of both residual rows (pieces 3h/2, 3h/2 + 1 and 3 + the same)
         const int ra = (p >> 3) & 1;
@@ -2462,28 +2464,36 @@ __global__ __launch_bounds__(kBlock) void k_pose_update(Dev d0) {
 // ---------------------------------------------------------------- edge-parallel trial path
 // per landmark: (Hll + λI) = L Lᵀ, g = L⁻¹ b_l (packed lower; recomputed where needed — 4x4,
 // cheaper than a kernel boundary)
-__device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, bool mul, double (&L)[10], double (&g)[4]) {
+// Signed form (the hand-rolled LM, `sgn`): (Hll + λ·diag) = M S Mᵀ with S = diag(±1), as an
+// unpivoted LDLᵀ tolerates a non-positive pivot (the reference solves the whole system with
+// SimplicialLDLT, src/mapHandler.cpp:1861-1865; a rank-deficient landmark block under λ·diag ≈
+// 1e-24·H meets one). Every sign is exactly 1 for a positive definite block, and the products
+// are grouped so that the result is then bitwise the plain Cholesky's.
+__device__ __forceinline__ void lm_chol(const Dev &d, int l, double lam, bool mul, double (&L)[10], double (&g)[4],
+                                        double (&S)[4], bool sgn = false) {
     const int DIM = is_point_lm(d, l) ? 3 : 4;
     double H[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) { H[k] = d.Hll[(size_t)l * 10 + k]; L[k] = 0.0; }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) g[k] = 0.0;
+    for (int k = 0; k < 4; ++k) { g[k] = 0.0; S[k] = 1.0; }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         if (j < DIM) {
             double sj = H[pk(j, j)] + (mul ? lam * H[pk(j, j)] : lam);
 #pragma unroll
-            for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
-            const double djj = 1.0 / sqrt(sj);  // reciprocal diagonal: every use divides by it
+            for (int p = 0; p < j; ++p) sj -= (L[pk(j, p)] * S[p]) * L[pk(j, p)];
+            const double sg = (sgn && sj < 0.0) ? -1.0 : 1.0;
+            S[j] = sg;
+            const double djj = 1.0 / sqrt(sg * sj);  // reciprocal diagonal: every use divides by it
             L[pk(j, j)] = djj;
 #pragma unroll
             for (int i = j + 1; i < 4; ++i) {
                 if (i < DIM) {
                     double t = H[pk(i, j)];
 #pragma unroll
-                    for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
-                    L[pk(i, j)] = t * djj;
+                    for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * (L[pk(j, p)] * S[p]);
+                    L[pk(i, j)] = (t * djj) * sg;
                 }
             }
         }
@@ -2547,8 +2557,9 @@ __device__ __forceinline__ void edge_schur_body(const Dev &d, int e, double *Z, 
         return;
     }
     const int DIM = e < d.Ep ? 3 : 4;
-    double L[10], g[4], B[8];
-    lm_chol(d, l, d.lam, d.ctrl->hlm != 0, L, g);
+    const bool sgn = d.ctrl->hlm == 1;
+    double L[10], g[4], B[8], S[4];
+    lm_chol(d, l, d.lam, d.ctrl->hlm != 0, L, g, S, sgn);
 #pragma unroll
     for (int k = 0; k < 8; ++k) B[k] = d.B[(size_t)e * 8 + k];
     double z[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -2564,12 +2575,21 @@ __device__ __forceinline__ void edge_schur_body(const Dev &d, int e, double *Z, 
             }
         }
     double q0 = 0, q1 = 0;
+    if (sgn) {  // hand-rolled LM (one live row): row 1 carries S·z_0, the assembly takes z_1·(S z_2)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        Z[i] = z[0][i];
-        Z[4 + i] = z[1][i];
-        q0 += z[0][i] * g[i];
-        q1 += z[1][i] * g[i];
+        for (int i = 0; i < 4; ++i) {
+            Z[i] = z[0][i];
+            Z[4 + i] = z[0][i] * S[i];
+            q0 += (z[0][i] * S[i]) * g[i];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            Z[i] = z[0][i];
+            Z[4 + i] = z[1][i];
+            q0 += z[0][i] * g[i];
+            q1 += z[1][i] * g[i];
+        }
     }
     qe[0] = q0;
     qe[1] = q1;
@@ -2789,7 +2809,9 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
         const bool first = c->iter == 0;
         int result = 0;
         c->hlm_solves += 1;
-        c->dx2 = scl[0];
+        const bool ok = __hip_atomic_load(&c->solve_ok[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        const double dx2 = ok ? scl[0] : 0.0;  // a failed solve leaves DX = 0 (|DX| < minchg stops)
+        c->dx2 = dx2;
         bool apply;
         if (first) {
             apply = true;
@@ -2801,7 +2823,6 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
             c->lambda *= c->hlm_k;
             apply = true;
         }
-        const bool ok = c->solve_ok[0] != 0;
         if (ok) c->last_ok = (c->last_ok + 1) % d.nbx;
         apply = apply && ok;  // (an LDLᵀ breakdown leaves X unchanged)
         if (apply) {
@@ -2813,7 +2834,7 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
                                                    c->lambda};
         c->iters_done[c->stage] += 1;
         c->iter += 1;
-        const bool small = !first && sqrt(scl[0]) < c->hlm_minchg;
+        const bool small = !first && sqrt(dx2) < c->hlm_minchg;
         c->err_prev = c->currentChi;
         if (small || c->iter >= c->max_iters[c->stage]) {
             c->chi2_final[c->stage] = c->currentChi;
@@ -3062,23 +3083,31 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
             const int DIM = pt ? 3 : 4;
             double x[4] = {0, 0, 0, 0};
             if (solve) {
-                // (Hll + λI) = L Lᵀ (packed lower), x = L⁻ᵀ L⁻¹ (b_l − u)
-                double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                // (Hll + λI) = L Lᵀ (packed lower), x = L⁻ᵀ L⁻¹ (b_l − u); the hand-rolled LM in
+                // the signed form of lm_chol, x = L⁻ᵀ S L⁻¹ (b_l − u)
+                const bool sgn = cg->hlm == 1;
+                double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, S[4] = {1.0, 1.0, 1.0, 1.0};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (j < DIM) {
                         double sj = H[pk(j, j)] + (hlm ? lam * H[pk(j, j)] : lam);
 #pragma unroll
-                        for (int p = 0; p < j; ++p) sj -= L[pk(j, p)] * L[pk(j, p)];
-                        const double djj = 1.0 / sqrt(sj);  // reciprocal diagonal (as lm_chol)
+                        for (int p = 0; p < j; ++p) sj -= (L[pk(j, p)] * S[p]) * L[pk(j, p)];
+                        const double sg = (sgn && sj < 0.0) ? -1.0 : 1.0;
+                        S[j] = sg;
+                        // a zero pivot fails the hand-rolled LM's solve (the oracle's unpivoted
+                        // LDLᵀ; the step is then not applied, k_decide's hlm branch)
+                        if (sgn && sj == 0.0)
+                            __hip_atomic_store(d.solve_okp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const double djj = 1.0 / sqrt(sg * sj);  // reciprocal diagonal (as lm_chol)
                         L[pk(j, j)] = djj;
 #pragma unroll
                         for (int i = j + 1; i < 4; ++i) {
                             if (i < DIM) {
                                 double t = H[pk(i, j)];
 #pragma unroll
-                                for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * L[pk(j, p)];
-                                L[pk(i, j)] = t * djj;
+                                for (int p = 0; p < j; ++p) t -= L[pk(i, p)] * (L[pk(j, p)] * S[p]);
+                                L[pk(i, j)] = (t * djj) * sg;
                             }
                         }
                     }
@@ -3092,6 +3121,8 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
                         for (int p = 0; p < i; ++p) t -= L[pk(i, p)] * y[p];
                         y[i] = t * L[pk(i, i)];
                     }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) y[i] *= S[i];
 #pragma unroll
                 for (int i = 3; i >= 0; --i)
                     if (i < DIM) {

@@ -68,6 +68,10 @@ CASES = [("C1", {}), ("C1L", {}), ("C2", {}),
          ("C1L", {"lambda0": 1e-24, "err_per_obs": 1}),
          ("C2", {"lambda0": 1e-24, "err_per_obs": 1}),
          ("C2", {"lambda0": 1e-24}),
+         # C1 at λ0 = 1e-24: an exactly zero landmark pivot fails the first two solves (DX = 0,
+         # X unchanged), with the finite and with the reference's infinite χ² (err_per_obs = 0)
+         ("C1", {"lambda0": 1e-24, "err_per_obs": 1}),
+         ("C1", {"lambda0": 1e-24}),
          ("C1", {"err_per_obs": 1, "max_iters": 4})]
 
 
