@@ -3037,6 +3037,8 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
                 double sj = H[pk(jj, jj)] + lam * H[pk(jj, jj)];
 #pragma unroll
                 for (int p = 0; p < jj; ++p) sj -= L6[pk(jj, p)] * L6[pk(jj, p)];
+                if (!(sj > 0.0))  // a non-positive pivot fails the solve (X unchanged, DX = 0)
+                    __hip_atomic_store(d.solve_okp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const double djj = sqrt(sj);
                 L6[pk(jj, jj)] = djj;
 #pragma unroll
@@ -3096,8 +3098,9 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
                         const double sg = (sgn && sj < 0.0) ? -1.0 : 1.0;
                         S[j] = sg;
                         // a zero pivot fails the hand-rolled LM's solve (the oracle's unpivoted
-                        // LDLᵀ; the step is then not applied, k_decide's hlm branch)
-                        if (sgn && sj == 0.0)
+                        // LDLᵀ; the step is then not applied, k_decide's hlm branch); GBA keeps
+                        // the Cholesky form and fails on any non-positive pivot
+                        if (hlm && (sgn ? sj == 0.0 : !(sj > 0.0)))
                             __hip_atomic_store(d.solve_okp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         const double djj = 1.0 / sqrt(sg * sj);  // reciprocal diagonal (as lm_chol)
                         L[pk(j, j)] = djj;
