@@ -40,6 +40,7 @@ import subprocess
 import sys
 import time
 
+T_START = time.perf_counter()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "pl-slam-plucker_amd"))
 
@@ -265,7 +266,7 @@ def shard_child(a, world: int):
             except ValueError:
                 continue
             keep = ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "scaling_reference",
-                    "final_chi2_gpu")
+                    "final_chi2_gpu", "comm")
             d = {k: r[k] for k in keep if k in r}
             d["workload"] = r.get("config", {}).get("workload")
             d["end_to_end"] = r.get("config", {}).get("end_to_end")
@@ -335,6 +336,10 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
+        # what the transport itself reports on every rank (RCCL's rank count / rank / device, the
+        # HIP device and its PCI location): the record proves N ranks ran on N distinct GPUs
+        from plba.dist import comm_summary, gather_comm_info
+        comm = gather_comm_info(s.comm_info()) if dist is not None else comm_summary([s.comm_info()])
     else:
         g = synth.generate(a.config, seed=base_seed + 97 * rank)
         t0 = time.perf_counter()
@@ -344,6 +349,7 @@ def main():
     s.upload(g)
     s.synchronize()
     upload_ms = (time.perf_counter() - t0) * 1e3
+    setup_s = time.perf_counter() - T_START  # process start -> window resident (shard-timeout budget)
 
     def step(with_trace=True):
         s.reset()
@@ -568,6 +574,14 @@ def main():
         out["final_chi2_gpu"] = [float(r["chi2"][0]), float(r["chi2"][1])]
         if ph is not None:
             out["phases"] = ph
+        if shard:
+            out["comm"] = {
+                **comm,
+                "setup_s_rank0": setup_s,
+                "note": "plba_comm_info on every rank (RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice; "
+                        "hipGetDevice and the PCI location of the context's device); setup_s = process start "
+                        "to the window resident on the device, incl. torch / RCCL init",
+            }
         if scaling_ref is not None:
             out["scaling_reference"] = scaling_ref
         if shard_run is not None:

@@ -143,8 +143,9 @@ int plba_enable_kernel_timing(plba_ctx *ctx, int32_t on);   /* HIP-event timing 
  * the column-lane factorisation (the context then keeps that factorisation), [17]=trial slots
  * a step evaluates at most (speculative damped trials, 1 = off), [18]=their policy
  * (0 off, 1 always, 2 after a rejection in the iteration, 3 after the first rejection of the
- * optimize() call), [19]=device steps the last schedule took, [20]=four-segment column-lane
- * factorisation (1/0), [21]=window structure built on the device (1) or on the host (0).
+ * optimize() call), [19]=device steps the last schedule took, [20]=unused (always 0; it was the
+ * four-segment column-lane factorisation, removed in round 5), [21]=window structure built on the
+ * device (1) or on the host (0).
  * Counts are this rank's when the window is sharded. */
 int plba_structure_stats(plba_ctx *ctx, int64_t *out, int32_t cap);
 int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *launches,
@@ -277,9 +278,11 @@ int plba_pgo_optimize(plba_ctx *ctx, const plba_pgo_graph *g, const plba_pgo_par
 /* ---- Sharded windows: one context per GPU, one window split over nranks.
  * Landmarks (with all their edges) are partitioned by the keyframe range of their first
  * observation (kf_obs_list[0], the base KF of map_points_kf_idx); poses are replicated.
- * Per LM trial each rank assembles its partial reduced camera system and the ranks sum it
- * with one all-reduce (plus a 42·nf-double all-reduce per outer iteration and a 2-double one
- * per trial); every rank then factorises the identical system redundantly, so accept/reject
+ * Per LM trial each rank assembles its partial reduced camera system and the ranks exchange it
+ * with one all-gather of each rank's block-row runs, summed in rank order (PLBA_SHARD_XCHG=allreduce:
+ * one all-reduce of the whole system), plus a 13·nf-double all-reduce per outer iteration and a
+ * 3-double one per trial (trial χ², scale, failed solves); every rank then factorises the identical
+ * system redundantly, so accept/reject
  * decisions agree bit for bit across ranks. plba_download / plba_get_edge_chi2 /
  * plba_lba_plucker return the FULL window on every rank (one final gather all-reduce).
  * Call exactly one plba_comm_init_* before plba_upload; every rank uploads the same full
@@ -295,6 +298,12 @@ int plba_comm_unique_id(uint8_t id[128]);
 int plba_comm_init_rccl(plba_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 /* Host transport (tests / hosts without RCCL): device buffers are staged through pinned memory. */
 int plba_comm_init_host(plba_ctx *ctx, int32_t nranks, int32_t rank, plba_host_allreduce_fn fn, void *user);
+/* What the transport itself reports, so that a multi-GPU record proves N ranks on N distinct GPUs:
+ * out[0] transport (0 none, 1 RCCL, 2 host), [1] ranks (RCCL: ncclCommCount), [2] this rank
+ * (RCCL: ncclCommUserRank), [3] the communicator's device (RCCL: ncclCommCuDevice; else the
+ * context's), [4] the HIP device ordinal the context runs on (hipGetDevice), [5] its PCI domain,
+ * [6] PCI bus, [7] PCI device. Entries past cap are not written. */
+int plba_comm_info(plba_ctx *ctx, int32_t *out, int32_t cap);
 
 #ifdef __cplusplus
 }

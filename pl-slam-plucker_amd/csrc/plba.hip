@@ -18,6 +18,7 @@
 #include <cstring>
 #include <limits>
 #include <map>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <type_traits>
@@ -124,6 +125,7 @@ struct plba_ctx {
     // context to the column-lane factorisation for good (no_bcr) and solve the window again
     bool no_bcr = false;
     int bcr_fallbacks = 0;
+    bool pool_hold = false;  // this context keeps the device pool's release threshold raised (prewarm)
     int dev_build = 0;  // the last upload's window structure was built on the device
     int fb_cl = 0, fb_twisted = 0, fb_tw_m = 0;  // the factorisation the window falls back to
     double *bk_T = nullptr, *bk_X = nullptr, *bk_xp = nullptr, *bk_xk = nullptr, *bk_Lpb = nullptr, *bk_XL = nullptr,
@@ -1270,10 +1272,10 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     ALLOC(d.trace, kTraceCap);
     ALLOC(ctx->d_depth, Ep);
     ALLOC(d.red_rcs, (size_t)nblk * 36 + (size_t)nf * 6);
-    ALLOC(d.red_dec, 2);
+    ALLOC(d.red_dec, 3);
     if (sharded) {
         ALLOC(d.red_rcs_loc, (size_t)nblk * 36 + (size_t)nf * 6);
-        ALLOC(d.red_dec_loc, 3);  // + the hand-off error agreement slot (agree_dev_error)
+        ALLOC(d.red_dec_loc, 4);  // + the hand-off error agreement slot (agree_dev_error)
     }
     d.xg_P = 0;
     d.xg_host = ctx->comm.kind == plba_ctx::Comm::HOST ? 1 : 0;
@@ -1494,7 +1496,7 @@ int launch_step(plba_ctx *ctx) {
     }
     if (d.sharded) {
         LAUNCH(K_PACK, hipLaunchKernelGGL(k_decide_pack, dim3(1), dim3(kBlock), 0, s, d));
-        COMM(d.red_dec_loc, d.red_dec, 2);
+        COMM(d.red_dec_loc, d.red_dec, 3);
     }
     if (!(d.fold && d.n_lm > 0))  // (folded into the last k_lm_solve workgroup otherwise)
         LAUNCH(K_DECIDE, hipLaunchKernelGGL(k_decide, dim3(1), dim3(kBlock), 0, s, d));
@@ -1628,7 +1630,7 @@ int bcr_state_copy(plba_ctx *ctx, bool save) {
 int agree_dev_error(plba_ctx *ctx, int mine, int *any) {
     *any = mine;
     if (!ctx->d.sharded) return PLBA_OK;
-    double *buf = ctx->d.red_dec_loc + 2;  // spare slot after the two decision sums
+    double *buf = ctx->d.red_dec_loc + 3;  // spare slot after the three decision terms
     const double v = mine ? 1.0 : 0.0;
     PLBA_CHECK(hipMemcpyAsync(buf, &v, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     int rc = allreduce(ctx, buf, buf, 1);
@@ -1878,6 +1880,36 @@ void plba_default_opts(plba_opts *o) {
     o->tau = 1e-5;
 }
 
+// The device's default memory pool is process-wide: its release threshold is raised while at
+// least one context of the device lives and the value found before the first one is put back when
+// the last one is destroyed (other users of the pool in the process see their own setting again).
+void pool_hold(plba_ctx *ctx, bool on) {
+    static std::mutex mu;
+    static std::map<int, std::pair<int, uint64_t>> held;  // device -> (contexts holding, previous threshold)
+    if (ctx->pool_hold == on) return;
+    std::lock_guard<std::mutex> lk(mu);
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, ctx->opts.device) != hipSuccess || !pool) {
+        (void)hipGetLastError();
+        return;
+    }
+    auto &h = held[ctx->opts.device];
+    if (on) {
+        if (h.first++ == 0) {
+            uint64_t prev = 0;
+            if (hipMemPoolGetAttribute(pool, hipMemPoolAttrReleaseThreshold, &prev) != hipSuccess) prev = 0;
+            h.second = prev;
+            uint64_t thr = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+    } else if (--h.first == 0) {
+        uint64_t prev = h.second;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &prev);
+    }
+    (void)hipGetLastError();
+    ctx->pool_hold = on;
+}
+
 // A three-keyframe window with points and a line solved once through the whole path (device
 // build, step graphs, every kernel of a step, output scatter); the context is left without a
 // window, as plba_create returns it.
@@ -1887,12 +1919,7 @@ int prewarm(plba_ctx *ctx) {
     // here (PLBA_PREWARM_MB, default 256 MB of the 288 GB), so that a first window does not pay
     // the pool's growth; the first pinned upload staging likewise.
     {
-        hipMemPool_t pool = nullptr;
-        if (hipDeviceGetDefaultMemPool(&pool, ctx->opts.device) == hipSuccess && pool) {
-            uint64_t thr = UINT64_MAX;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-        }
-        (void)hipGetLastError();
+        pool_hold(ctx, true);
         const char *mb = getenv("PLBA_PREWARM_MB");
         const size_t bytes = (size_t)(mb && mb[0] ? std::max(0, atoi(mb)) : 256) << 20;
         void *p = nullptr;
@@ -1993,12 +2020,21 @@ int plba_create(plba_ctx **out, const plba_opts *opts) {
     // code-object load, the first rocPRIM sorts of the device window build and the first pinned
     // staging (C3: first upload 38 ms against 1.2 ms warm) on the LBA thread's first keyframe.
     const char *npw = getenv("PLBA_NO_PREWARM");
+    // A failed pre-warm (a diagnostic switch in the caller's environment, say) is not fatal: the
+    // context is returned without a window, as it would be without the pre-warm, and the reason is
+    // kept in plba_last_error and printed once. A device that cannot run a kernel fails the caller's
+    // own first upload or solve instead.
     if (!(npw && npw[0] == '1')) {
         const int rc = prewarm(ctx);
         if (rc) {
-            plba_destroy(ctx);
-            *out = nullptr;
-            return rc;
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(ctx->stream);
+            ctx->uploaded = false;
+            ctx->initialized = false;
+            ctx->no_bcr = false;
+            ctx->bcr_fallbacks = 0;
+            ctx->set_error("pre-warm failed (%d): %s (continuing without it)", rc, ctx->err.c_str());
+            fprintf(stderr, "[plba] %s\n", ctx->err.c_str());
         }
     }
     return PLBA_OK;
@@ -2025,6 +2061,7 @@ int plba_destroy(plba_ctx *ctx) {
     if (ctx->comm.hbuf) (void)hipHostFree(ctx->comm.hbuf);
     if (ctx->comm.nccl) (void)ncclCommDestroy(ctx->comm.nccl);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    pool_hold(ctx, false);
     delete ctx;
     return PLBA_OK;
 }
@@ -2414,6 +2451,39 @@ int plba_comm_init_host(plba_ctx *ctx, int32_t nranks, int32_t rank, plba_host_a
     ctx->comm.rank = rank;
     ctx->comm.fn = fn;
     ctx->comm.user = user;
+    return PLBA_OK;
+}
+
+int plba_comm_info(plba_ctx *ctx, int32_t *out, int32_t cap) {
+    if (!ctx || (cap > 0 && !out)) return PLBA_E_INVALID;
+    (void)hipSetDevice(ctx->opts.device);
+    const auto &c = ctx->comm;
+    int32_t v[8] = {c.kind == plba_ctx::Comm::RCCL ? 1 : c.kind == plba_ctx::Comm::HOST ? 2 : 0,
+                    c.kind == plba_ctx::Comm::NONE ? 1 : c.nranks, c.rank, ctx->opts.device, -1, -1, -1, -1};
+    if (c.kind == plba_ctx::Comm::RCCL && c.nccl) {
+        int n = 0, r = 0, dv = 0;
+        if (ncclCommCount(c.nccl, &n) != ncclSuccess || ncclCommUserRank(c.nccl, &r) != ncclSuccess ||
+            ncclCommCuDevice(c.nccl, &dv) != ncclSuccess) {
+            ctx->set_error("RCCL communicator query failed");
+            return PLBA_E_COMM;
+        }
+        v[1] = n;
+        v[2] = r;
+        v[3] = dv;
+    }
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        ctx->set_error("hipGetDevice failed");
+        return PLBA_E_DEVICE;
+    }
+    v[4] = dev;
+    int a = 0;
+    if (hipDeviceGetAttribute(&a, hipDeviceAttributePciDomainID, dev) == hipSuccess) v[5] = a;
+    if (hipDeviceGetAttribute(&a, hipDeviceAttributePciBusId, dev) == hipSuccess) v[6] = a;
+    if (hipDeviceGetAttribute(&a, hipDeviceAttributePciDeviceId, dev) == hipSuccess) v[7] = a;
+    (void)hipGetLastError();
+    for (int i = 0; i < cap && i < 8; ++i) out[i] = v[i];
     return PLBA_OK;
 }
 

@@ -190,7 +190,7 @@ struct Dev {
     int64_t *xg_rng;
     int64_t xg_P;
     int32_t xg_host;
-    double *red_dec, *red_dec_loc;      // [2]: trial χ² | landmark part of Σx(λx+b)
+    double *red_dec, *red_dec_loc;      // [3]: trial χ² | landmark part of Σx(λx+b) | failed solves (sharded)
     double *Hpp_w, *bp_w;               // where pose_combine writes (== Hpp, bp unless sharded)
     // sharded: the iteration all-reduce carries only diag(Hpp) | b_p | active counts | scalars
     // (nf·13 + 2 + R); this rank's full partial Hpp (Hpp_w, local) rides in the RCS exchange inside
@@ -1899,7 +1899,12 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         }
       }
     };
-    if (!crit) stage_row(W, (tid >> 6) - 1, lane);
+    if (!crit) {
+        stage_row(W, (tid >> 6) - 1, lane);
+        // retired here like every later row's (the compiler does not track the inline-asm load,
+        // and step 0's phase 2 already copies its diagonal-BW block out of the staging buffer)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(tid) < 64) __builtin_amdgcn_s_setprio(3);
     // S_0^{-1}, y_0, z_0
@@ -2809,7 +2814,10 @@ __device__ __forceinline__ void decide_body(const Dev &d, double *sh) {
         const bool first = c->iter == 0;
         int result = 0;
         c->hlm_solves += 1;
-        const bool ok = __hip_atomic_load(&c->solve_ok[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        // sharded: the landmark pivots are checked on the rank that owns the landmark, so the
+        // decision uses the failures summed over the ranks (k_decide_pack), the same on every rank
+        const bool ok = d.sharded ? d.red_dec[2] == 0.0
+                                  : __hip_atomic_load(&c->solve_ok[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         const double dx2 = ok ? scl[0] : 0.0;  // a failed solve leaves DX = 0 (|DX| < minchg stops)
         c->dx2 = dx2;
         bool apply;
@@ -3210,6 +3218,9 @@ __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
     if (threadIdx.x == 0) {
         d.red_dec_loc[0] = ta;
         d.red_dec_loc[1] = tb;
+        // a failed solve on this rank (the hand-rolled LM's landmark pivots are rank-local): the
+        // ranks sum the failures so that every rank takes the same decision (decide_body)
+        d.red_dec_loc[2] = d.ctrl->solve_ok[0] != 0 ? 0.0 : 1.0;
     }
 }
 

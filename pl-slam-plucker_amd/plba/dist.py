@@ -53,3 +53,25 @@ def sharded_solver(device: int, transport: str = "rccl", group=None, rank: Optio
     else:
         raise ValueError(f"unknown transport {transport!r}")
     return s
+
+
+def comm_summary(infos: list) -> dict:
+    """Summary of every rank's Solver.comm_info(): the rank counts RCCL reports, whether the ranks
+    are 0..N-1 each once, and how many distinct devices (HIP ordinal + PCI location) they ran on."""
+    n = len(infos)
+    return {
+        "ranks": infos,
+        "rccl_ranks": sorted({int(c["ranks"]) for c in infos}),
+        "rank_set_ok": sorted(int(c["rank"]) for c in infos) == list(range(n))
+                       and all(int(c["ranks"]) == n for c in infos),
+        "distinct_hip_devices": len({(c["hip_device"], c["pci"]) for c in infos}),
+        "distinct_pci": len({c["pci"] for c in infos}),
+    }
+
+
+def gather_comm_info(info: dict, group=None) -> dict:
+    """All ranks' comm_info() gathered on every rank (gloo object all-gather), summarised."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, info, group=group)
+    return comm_summary(out)

@@ -27,6 +27,7 @@ EXPORTED = [
     "plba_refresh_edge_errors", "plba_get_edge_chi2", "plba_download", "plba_lba_plucker", "plba_get_trace",
     "plba_synchronize", "plba_enable_kernel_timing", "plba_kernel_times", "plba_structure_stats",
     "plba_shard_plan", "plba_comm_unique_id", "plba_comm_init_rccl", "plba_comm_init_host",
+    "plba_comm_info",
     "plba_hlm_default_params", "plba_hlm_lba",
     "plba_pgo_default_params", "plba_pgo_optimize",
 ]
@@ -78,6 +79,7 @@ def load(path: Optional[str] = None):
     L.plba_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
     L.plba_comm_init_rccl.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
     L.plba_comm_init_host.argtypes = [vp, C.c_int32, C.c_int32, HOST_ALLREDUCE_FN, vp]
+    L.plba_comm_info.argtypes = [vp, ip, C.c_int32]
     L.plba_hlm_default_params.argtypes = [C.POINTER(capi.PlbaHlmParams)]
     L.plba_hlm_default_params.restype = None
     L.plba_hlm_lba.argtypes = [vp, C.POINTER(capi.PlbaHlmState), C.POINTER(capi.PlbaHlmParams),
@@ -181,6 +183,15 @@ class Solver:
                 return -1
         self._host_cb = HOST_ALLREDUCE_FN(tramp)
         self._check(self.L.plba_comm_init_host(self.ctx, nranks, rank, self._host_cb, None), "plba_comm_init_host")
+
+    def comm_info(self) -> dict:
+        """What the transport reports (plba_comm_info): RCCL's own rank count, rank and device, and
+        the HIP device / PCI location this context runs on."""
+        v = np.zeros(8, np.int32)
+        self._check(self.L.plba_comm_info(self.ctx, _p(v, C.c_int32), 8), "plba_comm_info")
+        return dict(transport={0: "none", 1: "rccl", 2: "host"}.get(int(v[0]), str(int(v[0]))),
+                    ranks=int(v[1]), rank=int(v[2]), comm_device=int(v[3]), hip_device=int(v[4]),
+                    pci=f"{int(v[5]):04x}:{int(v[6]):02x}:{int(v[7]):02x}" if v[5] >= 0 else None)
 
     # -- g2o-style calls
     def upload(self, g: Graph):

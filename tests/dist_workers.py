@@ -81,6 +81,41 @@ def plan_and_schur_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
+def comm_info_worker(rank, world, port, outdir):
+    """CPU rank: what bench.py's sharded line records about the transport, gathered over gloo
+    (plba.dist.gather_comm_info) from a per-rank comm_info() as an RCCL rank on GPU `rank` would
+    report it."""
+    import json
+    dist = init_gloo(rank, world, port)
+    from plba.dist import gather_comm_info
+    info = dict(transport="rccl", ranks=world, rank=rank, comm_device=rank, hip_device=rank,
+                pci=f"0000:{0x11 + 0x20 * rank:02x}:00")
+    summ = gather_comm_info(info)
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump(summ, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def sharded_hlm_worker(rank, world, port, outdir, cfg, params):
+    """GPU rank: the hand-rolled LM on a sharded window over the host transport (a
+    landmark pivot that fails on one rank must fail the solve on every rank)."""
+    dist = init_gloo(rank, world, port)
+    from plba import capi, synth
+    from plba.dist import sharded_solver
+    from plba.hlm import hlm_window
+    win = hlm_window(synth.generate(cfg))
+    s = sharded_solver(device=0, transport="host")
+    info = s.comm_info()
+    s.upload(win.graph)
+    out = s.hlm_lba(win, capi.hlm_params(**params))
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"),
+             **out, info=np.array([info["ranks"], info["rank"], info["hip_device"]]))
+    s.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def sharded_gpu_worker(rank, world, port, outdir, cfg, transport, host_build=False, own_device=False):
     """GPU rank (all ranks may share one GPU with the host transport): full sharded LBA.
     host_build: PLBA_HOST_BUILD=1 (the host window build and its shard_plan) instead of the device

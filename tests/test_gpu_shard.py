@@ -145,11 +145,38 @@ def test_two_ranks_rccl_two_gpus_match_oracle(tmp_path, cfg):
     _check(r[0], oa.lba_plucker(synth.generate(cfg)))
 
 
+@pytest.mark.parametrize("cfg,params", [("C1", {"lambda0": 1e-24}), ("C1", {"lambda0": 1e-24, "err_per_obs": 1}),
+                                        ("C2", {})])
+def test_two_ranks_hand_rolled_lm_match_oracle(tmp_path, cfg, params):
+    """The hand-rolled LM on a sharded window (host transport). At λ0 = 1e-24 on C1 an exactly zero
+    landmark pivot fails the solve on the rank that owns the landmark only: the ranks sum their
+    failures in the decision all-reduce, so every rank rejects the step and stops together (ADVICE
+    r5; before, the other rank applied it and waited in the next collective)."""
+    import torch.multiprocessing as mp
+    from plba import capi
+    from plba.hlm import hlm_window
+    from test_gpu_hlm import _compare
+    world = 2
+    mp.spawn(dw.sharded_hlm_worker, args=(world, dw.free_port(), str(tmp_path), cfg, params), nprocs=world,
+             join=True)
+    r = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(world)]
+    for k in ("kf_x", "kf_Tcw", "pt_xyz", "ln_orth", "linearizations", "solves", "accepted", "trace"):
+        assert np.array_equal(r[0][k], r[1][k]), k
+    assert [list(x["info"]) for x in r] == [[world, 0, 0], [world, 1, 0]]
+    win = hlm_window(synth.generate(cfg))
+    ref = oa.hlm_lba(win, capi.hlm_params(**params))
+    out = {k: (v.item() if v.ndim == 0 else v) for k, v in r[0].items()}
+    _compare(out, ref, win)
+
+
 def test_one_rank_rccl_transport_matches_oracle():
     from plba.lib import Solver, comm_unique_id
     g = synth.generate("C1L")
     s = Solver()
     s.comm_init_rccl(1, 0, comm_unique_id())
+    ci = s.comm_info()
+    assert ci["transport"] == "rccl" and ci["ranks"] == 1 and ci["rank"] == 0, ci
+    assert ci["comm_device"] == ci["hip_device"] == 0 and ci["pci"], ci
     s.upload(g)
     out = s.lba_plucker()
     s.reset()

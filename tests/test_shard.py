@@ -54,3 +54,30 @@ def test_two_gloo_ranks_sum_partial_reduced_camera_systems(tmp_path):
     S, bs = dw.dense_schur_part(g, np.ones(g.n_pt, bool), np.ones(g.n_ln, bool))
     full = np.concatenate([S.ravel(), bs])
     np.testing.assert_allclose(r[0]["sum"], full, rtol=1e-10, atol=1e-8 * np.abs(full).max())
+
+
+def test_two_gloo_ranks_gather_the_transport_report(tmp_path):
+    """bench.py --mode shard records what the transport reports on every rank (plba_comm_info):
+    gathered over gloo, every rank holds the same summary, naming ranks 0..N-1 once each, the rank
+    count RCCL reported and the number of distinct GPUs (HIP ordinal + PCI location)."""
+    import json
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(dw.comm_info_worker, args=(world, dw.free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
+    assert r[0] == r[1]
+    s = r[0]
+    assert s["rank_set_ok"] and s["rccl_ranks"] == [world]
+    assert s["distinct_hip_devices"] == world and s["distinct_pci"] == world
+    assert [c["rank"] for c in s["ranks"]] == [0, 1] and [c["hip_device"] for c in s["ranks"]] == [0, 1]
+
+
+def test_comm_summary_flags_ranks_on_one_device():
+    """Two ranks that report the same device (the one-GPU host-transport rehearsal) count as one
+    distinct GPU; a rank set with a hole is not a valid N-rank communicator."""
+    from plba.dist import comm_summary
+    same = [dict(transport="host", ranks=2, rank=r, comm_device=0, hip_device=0, pci="0000:75:00") for r in (0, 1)]
+    s = comm_summary(same)
+    assert s["rank_set_ok"] and s["distinct_hip_devices"] == 1
+    bad = [dict(transport="rccl", ranks=3, rank=r, comm_device=r, hip_device=r, pci=f"0000:{r:02x}:00") for r in (0, 2)]
+    assert not comm_summary(bad)["rank_set_ok"]
