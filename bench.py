@@ -178,7 +178,7 @@ def concurrent_windows(a, dev: int, k: int):
                     "solved concurrently on one GPU (serving view; not the headline)"}
 
 
-def host_mirror(cfg: str, dev: int, calls: int = 3):
+def host_mirror(cfg: str, dev: int, calls: int = 3, background=None, scan_calls: int = 0):
     """The drop-in's whole per-call cost on the host mirror: the C++
     MapHandler::localBundleAdjustmentForPlukerWithG2O (src/mapHandler.cpp:5851-6323) on a synthetic
     map holding the config's window — gather + graph marshalling (:5868-6117), the device solve
@@ -187,22 +187,38 @@ def host_mirror(cfg: str, dev: int, calls: int = 3):
     does (outliers removed, fixed observers left local); the first call also creates the context."""
     from plba.slam_map import HostMap, make_map
     g = synth.generate(cfg)
+    t0 = time.perf_counter()
     hm = HostMap(make_map(g), device=dev)
-    rows = []
+    if background:   # (n_kf, n_pt, n_ln) of non-local map around the window
+        hm.add_background(*background, seed=11)
+    build_s = time.perf_counter() - t0
+
+    def summary(rows, mode):
+        warm = rows[1:]
+        med = {k: statistics.median(r[k] for r in warm)
+               for k in ("gather_ms", "upload_ms", "solve_ms", "bookkeeping_ms", "dirty_landmarks")}
+        return {"mode": mode, "gather_ms": med["gather_ms"], "upload_ms": med["upload_ms"],
+                "gather_plus_upload_ms": med["gather_ms"] + med["upload_ms"], "solve_ms": med["solve_ms"],
+                "outlier_and_writeback_ms": med["bookkeeping_ms"],
+                "total_ms": med["gather_ms"] + med["solve_ms"] + med["bookkeeping_ms"],
+                "dirty_landmarks": med["dirty_landmarks"],
+                "first_call_ms": rows[0]["gather_ms"] + rows[0]["solve_ms"] + rows[0]["bookkeeping_ms"], "calls": calls}
     try:
-        for _ in range(calls + 1):
-            rows.append(hm.local_ba())
+        rows = [hm.local_ba() for _ in range(calls + 1)]
+        out = summary(rows, "incremental")
+        if scan_calls:   # the same map, the reference's map-scanning gather (A/B)
+            hm.set_incremental(False)
+            out["scan"] = summary([hm.local_ba() for _ in range(scan_calls + 1)], "scan")
     finally:
         hm.close()
-    warm = rows[1:]
-    med = {k: statistics.median(r[k] for r in warm) for k in ("gather_ms", "solve_ms", "bookkeeping_ms")}
-    return {"gather_ms": med["gather_ms"], "solve_ms": med["solve_ms"], "outlier_and_writeback_ms": med["bookkeeping_ms"],
-            "total_ms": sum(med.values()), "first_call_ms": rows[0]["gather_ms"] + rows[0]["solve_ms"] + rows[0]["bookkeeping_ms"],
-            "calls": calls, "window": {k: rows[-1][k] for k in ("n_free_kf", "n_fixed_kf", "n_pt", "n_ln", "n_ept", "n_eln")},
-            "note": "median of calls 2..%d of MapHandler::localBundleAdjustmentForPlukerWithG2O (host/map_handler.cpp) "
-                    "on one synthetic map: gather = window gather + g2o-graph marshalling, solve = plba_upload + "
-                    "plba_lba_plucker incl. outputs (PCIe-inclusive), outlier_and_writeback = the outlier pass + "
-                    "pose/landmark write-back" % (calls + 1)}
+    out["map"] = {"keyframes": hm.n_kf, "points": hm.n_pt, "lines": hm.n_ln, "build_s": build_s}
+    out["window"] = {k: rows[-1][k] for k in ("n_free_kf", "n_fixed_kf", "n_pt", "n_ln", "n_ept", "n_eln")}
+    out["note"] = ("median of calls 2..%d of MapHandler::localBundleAdjustmentForPlukerWithG2O (host/map_handler.cpp) "
+                   "on one synthetic map: gather = window gather + g2o-graph marshalling (incremental: the local "
+                   "registry and cached observation runs; scan: the reference's scan of every map landmark), "
+                   "upload = plba_upload (part of solve), solve = plba_upload + plba_lba_plucker incl. outputs "
+                   "(PCIe-inclusive), outlier_and_writeback = the outlier pass + pose/landmark write-back" % (calls + 1))
+    return out
 
 
 def relaunch_distributed(a) -> int:
@@ -438,12 +454,19 @@ def main():
                            "speedup_of_this_run": (tot_iters / dt) / (ri / rdt), "phases": ref_ph}
         dist.barrier()
 
-    hmirror = None
+    hmirror = hmirror_map = None
     if world == 1 and not shard and not a.no_host_mirror:
         try:
             hmirror = host_mirror(a.config, dev)
         except Exception as e:  # informational: must never hide the single-window number
             hmirror = {"error": repr(e)}
+        if a.config == "C3":
+            # the same window inside a map of C5's size (BASELINE.json configs[4]: 1000 KF / 200k
+            # points / 40k lines), incremental gather and the reference's map scan on the same map
+            try:
+                hmirror_map = host_mirror(a.config, dev, background=(900, 180000, 36000), scan_calls=3)
+            except Exception as e:
+                hmirror_map = {"error": repr(e)}
 
     conc = None
     if world == 1 and not shard and a.windows > 1:
@@ -594,6 +617,8 @@ def main():
             out["concurrent_windows"] = conc
         if hmirror is not None:
             out["host_mirror"] = hmirror
+        if hmirror_map is not None:
+            out["host_mirror_c5_map"] = hmirror_map
         if world == 1 and not a.no_cpu_baseline:
             try:
                 cb = cpu_baseline(a.config, a.cpu_runs if a.config in ("C1", "C1L", "C2", "C3") else 1)

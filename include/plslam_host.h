@@ -44,6 +44,8 @@ typedef struct plslam_lba_stats {
     int32_t iters[2];
     double  chi2[2];
     double  gather_ms, solve_ms, bookkeeping_ms;
+    double  upload_ms;                     /* plba_upload, part of solve_ms (0 with a solver hook)   */
+    int32_t dirty_landmarks;               /* landmarks the incremental gather re-read from the map  */
 } plslam_lba_stats;
 
 int         plslam_map_create(plslam_map **m, double fx, double fy, double cx, double cy, const plba_opts *opts);
@@ -79,6 +81,16 @@ int plslam_kf_idx_get(plslam_map *m, int32_t kf, int32_t *out, int32_t cap, int3
 
 /* MapHandler::localBundleAdjustmentForPlukerWithG2O() */
 int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats);
+
+/* Incremental window (default on): the handler keeps every landmark's observations flattened and
+ * the local landmarks in a registry, so the LBA gather and formLocalMap cost O(window + changes)
+ * instead of scanning the map (the reference's :5877-5886, :1076-1091). Landmarks placed and
+ * changed through this ABI are tracked; a caller that writes a landmark's observations or position
+ * behind the handler's back reports it with plslam_mark_landmark_changed. on = 0: the scan gather.
+ * plslam_check_incremental_gather compares the landmark pass of both gathers (tests). */
+int plslam_set_incremental(plslam_map *m, int32_t on);
+int plslam_mark_landmark_changed(plslam_map *m, int32_t kind, int32_t idx);
+int plslam_check_incremental_gather(plslam_map *m, int32_t *equal);
 
 /* ---- MapHandler::localBundleAdjustmentForPluker() (src/mapHandler.cpp:1505-1615), the hand-rolled
  * LM of levMarquardtOptimizationLBAForPluker (:1618-2332) on the GPU (plba_hlm_lba), and its

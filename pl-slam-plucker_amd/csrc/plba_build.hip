@@ -44,8 +44,8 @@ struct Raw {  // the caller's graph, on the device
     const double *ept_obs, *ept_info, *eln_obs, *eln_info, *pt_xyz, *ln_orth;
     int n_kf, n_pt, n_ln, Ep, El;
 };
-// (vertex ids are validated by k_b_edges + a host check before any kernel below indexes with them;
-// the clamps only keep a broken input from ever addressing outside the arrays)
+// (vertex ids are validated by k_b_edges, reported at the stage's final read-back; the clamps keep
+// a broken input from ever addressing outside the arrays in the kernels that run before that)
 __device__ __forceinline__ void edge_of(const Raw &r, int e, int &lm, int &kf) {
     if (e < r.Ep) {
         lm = min(max(r.ept_lm[e], 0), max(r.n_pt - 1, 0));
@@ -427,15 +427,9 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
           s.pt_xyz, s.ln_orth, n_kf, np, nl, Ep, El};
     if (E) hipLaunchKernelGGL(k_b_edges, dim3(grid(E)), dim3(kNT), 0, st, r, s.first_e, s.cnt, s.lmin, s.err);
     BCHECK(hipGetLastError());
-    // every later kernel indexes through the edges' vertex ids: stop here on an invalid edge
-    int32_t bad = kBig;
-    BCHECK(hipMemcpyAsync(&bad, s.err, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    BCHECK(hipStreamSynchronize(st));
-    if (bad != kBig) {
-        wb.invalid = true;
-        snprintf(err, errlen, "%s edge %d references a missing vertex", bad < Ep ? "point" : "line", bad < Ep ? bad : bad - Ep);
-        return PLBA_E_INVALID;
-    }
+    // An invalid edge is reported at the final read-back: every later kernel reads vertex ids
+    // through edge_of's clamps, so a broken input never addresses outside the arrays (its build is
+    // discarded); no round trip to the host in the middle of the stage.
     hipLaunchKernelGGL(k_b_iota, dim3(grid(nf)), dim3(kNT), 0, st, s.first_blk, nf);
     if (E && nf)
         hipLaunchKernelGGL(k_b_first_blk, dim3((unsigned)std::min<int64_t>(grid(E), 64)), dim3(kNT), 0, st, r, s.lmin,
@@ -490,10 +484,17 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
     BCHECK(hipGetLastError());
     // ---- read back the counts, the first invalid edge and the envelope
     int32_t sum[8] = {0};
+    int32_t bad = kBig;
     wb.first_blk.assign(nf, 0);
     BCHECK(hipMemcpyAsync(sum, s.summary, sizeof(int32_t) * 5, hipMemcpyDeviceToHost, st));
+    BCHECK(hipMemcpyAsync(&bad, s.err, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (nf) BCHECK(hipMemcpyAsync(wb.first_blk.data(), s.first_blk, sizeof(int32_t) * nf, hipMemcpyDeviceToHost, st));
     BCHECK(hipStreamSynchronize(st));
+    if (bad != kBig) {
+        wb.invalid = true;
+        snprintf(err, errlen, "%s edge %d references a missing vertex", bad < Ep ? "point" : "line", bad < Ep ? bad : bad - Ep);
+        return PLBA_E_INVALID;
+    }
     wb.n_pt = sum[0];
     wb.n_ln = sum[1];
     wb.n_lm = sum[0] + sum[1];

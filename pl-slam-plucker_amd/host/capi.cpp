@@ -2,6 +2,7 @@
 #include "plslam_host.h"
 
 #include <cstring>
+#include <string>
 #include <new>
 
 #include "plslam_map.hpp"
@@ -71,6 +72,7 @@ int plslam_add_point(plslam_map *m, int32_t idx, const double xyz[3], const uint
     place(m->mh.map_points, idx,
           new MapPoint(idx, Vec3{xyz[0], xyz[1], xyz[2]}, make_desc(desc, desc_bytes), kf, Vec2{obs[0], obs[1]}, d,
                        sigma2));
+    m->mh.adoptLandmark(1, idx);
     return PLBA_OK;
 }
 
@@ -90,6 +92,7 @@ int plslam_add_line(plslam_map *m, int32_t idx, const double NDw[6], const uint8
     std::memcpy(L.data(), NDw, sizeof(double) * 6);
     place(m->mh.map_lines, idx,
           new MapLine(idx, L, make_desc(desc, desc_bytes), kf, Vec4{obs[0], obs[1], obs[2], obs[3]}, sigma2));
+    m->mh.adoptLandmark(2, idx);
     return PLBA_OK;
 }
 
@@ -109,13 +112,8 @@ int plslam_set_local(plslam_map *m, int32_t kind, int32_t idx, int32_t local) {
             m->mh.map_keyframes[idx]->local = local != 0;
             return PLBA_OK;
         case 1:
-            if (!slot_ok(m->mh.map_points, idx)) return PLBA_E_INVALID;
-            m->mh.map_points[idx]->local = local != 0;
-            return PLBA_OK;
         case 2:
-            if (!slot_ok(m->mh.map_lines, idx)) return PLBA_E_INVALID;
-            m->mh.map_lines[idx]->local = local != 0;
-            return PLBA_OK;
+            return m->mh.setLandmarkLocal(kind, idx, local != 0);
         default:
             return PLBA_E_INVALID;
     }
@@ -177,7 +175,31 @@ static void copy_stats(const LbaStats &st, plslam_lba_stats *stats) {
         stats->iters[0] = st.iters[0]; stats->iters[1] = st.iters[1];
         stats->chi2[0] = st.chi2[0]; stats->chi2[1] = st.chi2[1];
         stats->gather_ms = st.gather_ms; stats->solve_ms = st.solve_ms; stats->bookkeeping_ms = st.bookkeeping_ms;
+        stats->upload_ms = st.upload_ms;
+        stats->dirty_landmarks = st.dirty_landmarks;
     }
+}
+
+int plslam_set_incremental(plslam_map *m, int32_t on) {
+    if (!m) return PLBA_E_INVALID;
+    m->mh.incremental = on != 0;
+    m->mh.rebuildLocalRegistry();
+    return PLBA_OK;
+}
+
+int plslam_mark_landmark_changed(plslam_map *m, int32_t kind, int32_t idx) {
+    if (!m || (kind != 1 && kind != 2) || idx < 0) return PLBA_E_INVALID;
+    m->mh.markLandmarkChanged(kind, idx);
+    return PLBA_OK;
+}
+
+int plslam_check_incremental_gather(plslam_map *m, int32_t *equal) {
+    if (!m || !equal) return PLBA_E_INVALID;
+    std::string why;
+    const int rc = m->mh.checkIncrementalGather(&why);
+    *equal = rc == 0 ? 1 : 0;
+    if (rc) m->mh.setError("incremental gather differs from the scan gather: %s", why.c_str());
+    return PLBA_OK;
 }
 
 int plslam_local_ba_plucker_g2o(plslam_map *m, plslam_lba_stats *stats) {

@@ -294,6 +294,7 @@ int MapHandler::loopClosurePGO(bool ess, PgoStats *stats) {
                 if (idx < 0 || idx >= (int)map_points.size() || map_points[idx] == nullptr) continue;
                 MapPoint *mp = map_points[idx];
                 mp->point3D = xform(Tkfw_corr, mp->point3D);
+                markLandmarkChanged(1, idx);
                 mp->med_obs_dir = xform(Tkfw_corr, mp->med_obs_dir);  // directions get the translation too
                 for (Vec3 &d : mp->dir_list) d = xform(Tkfw_corr, d);
             }

@@ -3,13 +3,31 @@
 #include "plslam_map.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <memory>
+
+#include <omp.h>
 
 namespace plslam {
+
+// Threads for the per-element passes of one LBA call (gather copies, remaps, write-back), when the
+// pass is long enough to pay for the fork/join (the pool persists across calls): up to 8
+// (PLSLAM_THREADS overrides; 1 = serial). C3 window in a C5-sized map on the GPU box's host:
+// gather 0.66 -> 0.43 ms, write-back 1.09 -> 0.28 ms with 8.
+static int pass_threads(size_t n) {
+    static const int cap = [] {
+        const char *e = getenv("PLSLAM_THREADS");
+        return e ? std::max(1, atoi(e)) : 8;
+    }();
+    if (cap == 1 || n < 32768) return 1;
+    return std::max(1, std::min(cap, omp_get_max_threads()));
+}
 
 // ----------------------------------------------------------------------------- helpers
 int hamming(const Desc &a, const Desc &b) {  // cv::norm(a, b, NORM_HAMMING)
@@ -61,6 +79,51 @@ Mat4 inverse4(const Mat4 &m) {
     return inv;
 }
 
+// ----------------------------------------------------------------------------- incremental window
+// Per landmark slot: its observations flattened into an arena (observer kf_idx, observation,
+// (float)(1/σ²) as the reference's const float& reads it, index in the landmark's lists), its
+// position as the gather hands it over (point3D; changePlukerToOrth(NDw) for lines) and whether it
+// is in the local registry. Runs are rewritten (appended) when the landmark changes and the arena
+// is compacted when garbage exceeds the live edges.
+struct LmEntry {
+    int32_t off = -1, n = 0, idx = -1;  // arena run; the object's idx field
+    uint8_t dirty = 0, local = 0;
+    double pos[4] = {0, 0, 0, 0};
+};
+struct LmSide {
+    int ow;                              // observation doubles per edge (2 points, 4 lines)
+    std::vector<LmEntry> e;
+    std::vector<int32_t> a_kf, a_oi;
+    std::vector<double> a_obs, a_info;
+    size_t live = 0;
+    std::vector<int32_t> reg;            // local registry (slot indices; sorted + filtered lazily)
+    bool reg_sorted = true;
+    explicit LmSide(int w) : ow(w) {}
+    LmEntry &at(int idx) {
+        if ((int)e.size() <= idx) e.resize((size_t)idx + 1);
+        return e[idx];
+    }
+    void clear() {
+        e.clear(); a_kf.clear(); a_oi.clear(); a_obs.clear(); a_info.clear(); reg.clear();
+        live = 0;
+        reg_sorted = true;
+    }
+};
+struct LandmarkStore {
+    bool active = true;
+    LmSide pt{2}, ln{4};
+    std::vector<std::pair<int8_t, int32_t>> log;  // changed landmarks since the last gather
+    LmSide &side(int kind) { return kind == 1 ? pt : ln; }
+};
+void landmark_changed(LandmarkStore *s, int kind, int idx) {
+    if (!s || !s->active || idx < 0 || (kind != 1 && kind != 2)) return;
+    LmEntry &en = s->side(kind).at(idx);
+    if (!en.dirty) {
+        en.dirty = 1;
+        s->log.push_back({(int8_t)kind, idx});
+    }
+}
+
 // ----------------------------------------------------------------------------- MapPoint
 MapPoint::MapPoint(int idx_, const Vec3 &p, const Desc &desc, int kf_obs, const Vec2 &obs, const Vec3 &dir,
                    double sigma2)
@@ -82,6 +145,7 @@ void MapPoint::addMapPointObservation(const Desc &desc, int kf_obs, const Vec2 &
     dir_list.push_back(dir);
     sigma_list.push_back(sigma2);
     updateAverageDescDir();
+    landmark_changed(store, 1, idx);
 }
 
 // Index of the descriptor with the smallest median Hamming distance to the others
@@ -139,6 +203,7 @@ void MapLine::addMapLineObservation(const Desc &desc, int kf_obs, const Vec4 &ob
     sigma_list.push_back(sigma2);
     kf_obs_list.push_back(kf_obs);
     updateAverageDescDir();
+    landmark_changed(store, 2, idx);
 }
 
 void MapLine::updateAverageDescDir() {  // src/mapFeatures.cpp:140-184 (USE_LINE_PLUKER)
@@ -213,7 +278,7 @@ plba_graph Window::graph(double fx, double fy, double cx, double cy) const {
 
 // ----------------------------------------------------------------------------- MapHandler
 MapHandler::MapHandler(double fx, double fy, double cx, double cy, const plba_opts *opts)
-    : fx_(fx), fy_(fy), cx_(cx), cy_(cy) {
+    : store_(new LandmarkStore()), fx_(fx), fy_(fy), cx_(cx), cy_(cy) {
     if (opts) {
         opts_ = *opts;
         have_opts_ = true;
@@ -243,8 +308,29 @@ static bool has_duplicate_id(const Window &w);
 // pass over the observations: the per-edge arrays are written with observer ids while the ids
 // are validated and the observers marked; the map is mutated (fixed observers become local) only
 // once every observation is known valid, and the ids are then remapped to kf positions.
+// The landmark pass scans the map (gatherScan, as the reference) or walks the local registry and
+// copies each landmark's cached run (gatherIncremental); both produce the same arrays.
 int MapHandler::gatherWindow(Window &w) {
+    const auto t0 = std::chrono::steady_clock::now();
     w.clear();
+    std::vector<uint8_t> observer(map_keyframes.size(), 0);
+    int dirty = 0;
+    const int rc = incremental ? gatherIncremental(w, observer, &dirty) : gatherScan(w, observer);
+    last_dirty_ = dirty;
+    if (rc) {
+        w.clear();
+        return rc;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    const int rc2 = finishGather(w, observer);
+    if (getenv("PLSLAM_TIMING"))
+        fprintf(stderr, "[plslam gather] landmarks %.3f ms, keyframes + remap %.3f ms\n",
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+    return rc2;
+}
+
+int MapHandler::gatherScan(Window &w, std::vector<uint8_t> &observer) {
     const int nkf_map = (int)map_keyframes.size();
     std::vector<uint8_t> valid(nkf_map, 0);
     for (int o = 0; o < nkf_map; ++o) valid[o] = map_keyframes[o] && map_keyframes[o]->kf_idx == o;
@@ -276,7 +362,6 @@ int MapHandler::gatherWindow(Window &w) {
     w.eln_obs_idx.resize(n_eln);
     // The landmark passes read the map only: an invalid observation ends the gather before the
     // map is touched (the reference exit(0)s, :5891-5895, 5907-5911).
-    std::vector<uint8_t> observer(nkf_map, 0);
     // point vertices + edges (:5976-6027); ept_kf holds the observer id until the remap below
     for (size_t li = 0, e = 0; li < npt; ++li) {
         MapPoint *p = w.local_pt[li];
@@ -287,7 +372,6 @@ int MapHandler::gatherWindow(Window &w) {
             const int kf_id = p->kf_obs_list[i];
             if (kf_id < 0 || kf_id >= nkf_map || !valid[kf_id]) {
                 setError("[Wrong index in the map_keyframes and MapPoint obs] point %d obs kf %d", p->idx, kf_id);
-                w.clear();
                 return PLBA_E_INVALID;
             }
             observer[kf_id] = 1;
@@ -309,7 +393,6 @@ int MapHandler::gatherWindow(Window &w) {
             const int kf_id = l->kf_obs_list[i];
             if (kf_id < 0 || kf_id >= nkf_map || !valid[kf_id]) {
                 setError("[Wrong index in the map_keyframes and MapLine obs] line %d obs kf %d", l->idx, kf_id);
-                w.clear();
                 return PLBA_E_INVALID;
             }
             observer[kf_id] = 1;
@@ -323,7 +406,274 @@ int MapHandler::gatherWindow(Window &w) {
         const Vec4 o = MapLine::changePlukerToOrth(l->NDw);
         for (int k = 0; k < 4; ++k) w.ln_orth[li * 4 + k] = o[k];
     }
+    return PLBA_OK;
+}
 
+// Rewrites one landmark's cached run from its object (or clears it: slot empty).
+static void flatten(LandmarkStore &S, int kind, int idx, MapPoint *p, MapLine *l) {
+    LmSide &sd = S.side(kind);
+    LmEntry &en = sd.at(idx);
+    en.dirty = 0;
+    sd.live -= (size_t)en.n;
+    en.off = -1;
+    en.n = 0;
+    if (!p && !l) {
+        en.local = 0;
+        return;
+    }
+    const std::vector<int> &kfl = p ? p->kf_obs_list : l->kf_obs_list;
+    const std::vector<double> &sig = p ? p->sigma_list : l->sigma_list;
+    const int n = (int)kfl.size();
+    en.off = (int32_t)sd.a_kf.size();
+    en.n = n;
+    en.idx = p ? p->idx : l->idx;
+    for (int i = 0; i < n; ++i) {
+        sd.a_kf.push_back(kfl[i]);
+        sd.a_oi.push_back(i);
+        const float invSigma2 = 1.0 / sig[i];  // const float& (:6009, :6073)
+        sd.a_info.push_back((double)invSigma2);
+        if (p) {
+            sd.a_obs.push_back(p->obs_list[i][0]);
+            sd.a_obs.push_back(p->obs_list[i][1]);
+        } else {
+            for (int k = 0; k < 4; ++k) sd.a_obs.push_back(l->NDw_obs_list[i][k]);
+        }
+    }
+    sd.live += (size_t)n;
+    if (p) {
+        for (int k = 0; k < 3; ++k) en.pos[k] = p->point3D[k];
+    } else {
+        const Vec4 o = MapLine::changePlukerToOrth(l->NDw);
+        for (int k = 0; k < 4; ++k) en.pos[k] = o[k];
+    }
+}
+
+// arena garbage (runs rewritten since) above the live edges: copy the live runs, slot order
+static void compact(LmSide &sd) {
+    if (sd.a_kf.size() <= 2 * sd.live + (1u << 16)) return;
+    std::vector<int32_t> kf, oi;
+    std::vector<double> obs, info;
+    kf.reserve(sd.live); oi.reserve(sd.live); info.reserve(sd.live); obs.reserve(sd.live * sd.ow);
+    for (LmEntry &en : sd.e) {
+        if (en.off < 0) continue;
+        const int32_t off = (int32_t)kf.size();
+        kf.insert(kf.end(), sd.a_kf.begin() + en.off, sd.a_kf.begin() + en.off + en.n);
+        oi.insert(oi.end(), sd.a_oi.begin() + en.off, sd.a_oi.begin() + en.off + en.n);
+        info.insert(info.end(), sd.a_info.begin() + en.off, sd.a_info.begin() + en.off + en.n);
+        obs.insert(obs.end(), sd.a_obs.begin() + (size_t)en.off * sd.ow, sd.a_obs.begin() + (size_t)(en.off + en.n) * sd.ow);
+        en.off = off;
+    }
+    sd.a_kf.swap(kf); sd.a_oi.swap(oi); sd.a_obs.swap(obs); sd.a_info.swap(info);
+}
+
+int MapHandler::gatherIncremental(Window &w, std::vector<uint8_t> &observer, int *dirty) {
+    LandmarkStore &S = *store_;
+    const int nkf_map = (int)map_keyframes.size();
+    std::vector<uint8_t> valid(nkf_map, 0);
+    for (int o = 0; o < nkf_map; ++o) valid[o] = map_keyframes[o] && map_keyframes[o]->kf_idx == o;
+    // the landmarks that changed since the last gather (and local ones never cached)
+    int nd = 0;
+    auto obj = [&](int kind, int idx, MapPoint *&p, MapLine *&l) {
+        p = nullptr;
+        l = nullptr;
+        if (kind == 1 && idx < (int)map_points.size()) p = map_points[idx];
+        if (kind == 2 && idx < (int)map_lines.size()) l = map_lines[idx];
+    };
+    for (const auto &c : S.log) {
+        MapPoint *p;
+        MapLine *l;
+        obj(c.first, c.second, p, l);
+        flatten(S, c.first, c.second, p, l);
+        ++nd;
+    }
+    S.log.clear();
+    for (int kind = 1; kind <= 2; ++kind) {
+        LmSide &sd = S.side(kind);
+        if (!sd.reg_sorted) {
+            std::sort(sd.reg.begin(), sd.reg.end());
+            sd.reg.erase(std::unique(sd.reg.begin(), sd.reg.end()), sd.reg.end());
+            sd.reg_sorted = true;
+        }
+        size_t o = 0;
+        for (int32_t idx : sd.reg) {
+            MapPoint *p;
+            MapLine *l;
+            obj(kind, idx, p, l);
+            LmEntry &en = sd.at(idx);
+            if ((!p && !l) || !en.local) {
+                en.local = 0;
+                continue;
+            }
+            if (en.off < 0) {
+                flatten(S, kind, idx, p, l);
+                ++nd;
+            }
+            sd.reg[o++] = idx;
+        }
+        sd.reg.resize(o);
+        compact(sd);
+    }
+    *dirty = nd;
+    size_t n_ept = 0, n_eln = 0;
+    for (int32_t idx : S.pt.reg) n_ept += (size_t)S.pt.e[idx].n;
+    for (int32_t idx : S.ln.reg) n_eln += (size_t)S.ln.e[idx].n;
+    const size_t npt = S.pt.reg.size(), nln = S.ln.reg.size();
+    w.local_pt.resize(npt);
+    w.local_ls.resize(nln);
+    w.pt_id.resize(npt);
+    w.pt_xyz.resize(npt * 3);
+    w.ept_lm.resize(n_ept);
+    w.ept_kf.resize(n_ept);
+    w.ept_obs.resize(n_ept * 2);
+    w.ept_info.resize(n_ept);
+    w.ept_obs_idx.resize(n_ept);
+    w.ln_id.resize(nln);
+    w.ln_orth.resize(nln * 4);
+    w.eln_lm.resize(n_eln);
+    w.eln_kf.resize(n_eln);
+    w.eln_obs.resize(n_eln * 4);
+    w.eln_info.resize(n_eln);
+    w.eln_obs_idx.resize(n_eln);
+    // point vertices + edges (:5976-6027) then line vertices + edges (:6029-6117), from the cached
+    // runs (memcpy per run; raw pointers: the vectors' storage does not move in the loop);
+    // ept_kf / eln_kf hold the observer ids until finishGather
+    // edge offset of every registered landmark (the runs are copied in parallel)
+    std::vector<size_t> pt_e0(npt + 1, 0), ln_e0(nln + 1, 0);
+    for (size_t li = 0; li < npt; ++li) pt_e0[li + 1] = pt_e0[li] + (size_t)S.pt.e[S.pt.reg[li]].n;
+    for (size_t li = 0; li < nln; ++li) ln_e0[li + 1] = ln_e0[li] + (size_t)S.ln.e[S.ln.reg[li]].n;
+    auto pass = [&](LmSide &sd, int ow, int pw, const std::vector<int32_t> &reg, const std::vector<size_t> &e0,
+                    auto *objs, auto &local_out, int32_t *ids, double *pos, int32_t *lm, int32_t *kfo, double *obs,
+                    double *info, int *oidx, const char *what) -> int {
+        const int32_t *a_kf = sd.a_kf.data(), *a_oi = sd.a_oi.data();
+        const double *a_obs = sd.a_obs.data(), *a_info = sd.a_info.data();
+        const LmEntry *ent = sd.e.data();
+        const uint8_t *vld = valid.data();
+        uint8_t *obsr = observer.data();
+        std::atomic<int64_t> first_bad{INT64_MAX};  // (landmark << 32 | observation) of the first invalid one
+        const int64_t nreg = (int64_t)reg.size();
+#pragma omp parallel for schedule(static) num_threads(pass_threads(e0.back()))
+        for (int64_t li = 0; li < nreg; ++li) {
+            const int32_t idx = reg[li];
+            const LmEntry &en = ent[idx];
+            local_out[li] = objs[idx];
+            ids[li] = en.idx;
+            for (int k = 0; k < pw; ++k) pos[li * pw + k] = en.pos[k];
+            const size_t a = (size_t)en.off, n = (size_t)en.n, e = e0[li];
+            // (runs are ~5 edges: element loops, a memcpy call per run costs more than the copy)
+            for (size_t i = 0; i < n; ++i) {
+                const int kf_id = a_kf[a + i];
+                if (kf_id < 0 || kf_id >= nkf_map || !vld[kf_id]) {
+                    int64_t cur = first_bad.load(std::memory_order_relaxed), mine = (li << 32) | (int64_t)i;
+                    while (mine < cur && !first_bad.compare_exchange_weak(cur, mine)) {}
+                    break;
+                }
+                if (!__atomic_load_n(&obsr[kf_id], __ATOMIC_RELAXED))  // (written once per KF: no line ping-pong)
+                    __atomic_store_n(&obsr[kf_id], (uint8_t)1, __ATOMIC_RELAXED);
+                lm[e + i] = (int32_t)li;
+                kfo[e + i] = kf_id;
+                info[e + i] = a_info[a + i];
+                oidx[e + i] = a_oi[a + i];
+                for (int k = 0; k < ow; ++k) obs[(e + i) * ow + k] = a_obs[(a + i) * ow + k];
+            }
+        }
+        const int64_t bad = first_bad.load();
+        if (bad != INT64_MAX) {  // the scan gather's message: the first invalid observation in map order
+            const LmEntry &en = ent[reg[bad >> 32]];
+            setError("[Wrong index in the map_keyframes and %s obs] %s %d obs kf %d", what, ow == 2 ? "point" : "line",
+                     en.idx, a_kf[(size_t)en.off + (bad & 0xffffffff)]);
+            return PLBA_E_INVALID;
+        }
+        return PLBA_OK;
+    };
+    int rc = pass(S.pt, 2, 3, S.pt.reg, pt_e0, map_points.data(), w.local_pt, w.pt_id.data(), w.pt_xyz.data(),
+                  w.ept_lm.data(), w.ept_kf.data(), w.ept_obs.data(), w.ept_info.data(), w.ept_obs_idx.data(), "MapPoint");
+    if (!rc)
+        rc = pass(S.ln, 4, 4, S.ln.reg, ln_e0, map_lines.data(), w.local_ls, w.ln_id.data(), w.ln_orth.data(),
+                  w.eln_lm.data(), w.eln_kf.data(), w.eln_obs.data(), w.eln_info.data(), w.eln_obs_idx.data(), "MapLine");
+    return rc;
+}
+
+void MapHandler::adoptLandmark(int kind, int idx) {
+    if (kind == 1 && idx >= 0 && idx < (int)map_points.size() && map_points[idx]) map_points[idx]->store = store_.get();
+    if (kind == 2 && idx >= 0 && idx < (int)map_lines.size() && map_lines[idx]) map_lines[idx]->store = store_.get();
+    if (!store_->active) return;
+    LmSide &sd = store_->side(kind);
+    LmEntry &en = sd.at(idx);
+    const bool loc = kind == 1 ? map_points[idx] && map_points[idx]->local : map_lines[idx] && map_lines[idx]->local;
+    if (loc && !en.local) {
+        sd.reg.push_back(idx);
+        sd.reg_sorted = false;
+    }
+    en.local = loc ? 1 : 0;
+    landmark_changed(store_.get(), kind, idx);
+}
+
+void MapHandler::markLandmarkChanged(int kind, int idx) { landmark_changed(store_.get(), kind, idx); }
+
+int MapHandler::setLandmarkLocal(int kind, int idx, bool local) {
+    if (kind == 1) {
+        if (idx < 0 || idx >= (int)map_points.size() || !map_points[idx]) return PLBA_E_INVALID;
+        map_points[idx]->local = local;
+    } else if (kind == 2) {
+        if (idx < 0 || idx >= (int)map_lines.size() || !map_lines[idx]) return PLBA_E_INVALID;
+        map_lines[idx]->local = local;
+    } else {
+        return PLBA_E_INVALID;
+    }
+    if (!store_->active) return PLBA_OK;
+    LmSide &sd = store_->side(kind);
+    LmEntry &en = sd.at(idx);
+    if (local && !en.local) {
+        sd.reg.push_back(idx);
+        sd.reg_sorted = false;
+    }
+    en.local = local ? 1 : 0;  // (a cleared entry leaves the registry at the next gather)
+    return PLBA_OK;
+}
+
+// The store rebuilt from the map: every landmark adopted, the registry = the local flags.
+void MapHandler::rebuildLocalRegistry() {
+    LandmarkStore &S = *store_;
+    S.pt.clear();
+    S.ln.clear();
+    S.log.clear();
+    S.active = incremental;
+    for (size_t i = 0; i < map_points.size(); ++i)
+        if (map_points[i]) adoptLandmark(1, (int)i);
+    for (size_t i = 0; i < map_lines.size(); ++i)
+        if (map_lines[i]) adoptLandmark(2, (int)i);
+}
+
+// Tests: the landmark pass of the scan gather and of the incremental gather, compared array by
+// array (the map is not mutated: the KF part is not run).
+int MapHandler::checkIncrementalGather(std::string *why) {
+    Window a, b;
+    std::vector<uint8_t> oa(map_keyframes.size(), 0), ob(map_keyframes.size(), 0);
+    const int ra = gatherScan(a, oa);
+    int nd = 0;
+    const int rb = gatherIncremental(b, ob, &nd);
+    auto fail = [&](const char *what) {
+        if (why) *why = what;
+        return 1;
+    };
+    if (ra != rb) return fail("status");
+    if (ra) return PLBA_OK;
+    if (oa != ob) return fail("observers");
+    if (a.local_pt != b.local_pt || a.local_ls != b.local_ls) return fail("landmark sets");
+    if (a.pt_id != b.pt_id || a.ln_id != b.ln_id) return fail("ids");
+    if (a.pt_xyz != b.pt_xyz || a.ln_orth != b.ln_orth) return fail("positions");
+    if (a.ept_lm != b.ept_lm || a.ept_kf != b.ept_kf || a.ept_obs != b.ept_obs || a.ept_info != b.ept_info ||
+        a.ept_obs_idx != b.ept_obs_idx)
+        return fail("point edges");
+    if (a.eln_lm != b.eln_lm || a.eln_kf != b.eln_kf || a.eln_obs != b.eln_obs || a.eln_info != b.eln_info ||
+        a.eln_obs_idx != b.eln_obs_idx)
+        return fail("line edges");
+    return PLBA_OK;
+}
+
+int MapHandler::finishGather(Window &w, const std::vector<uint8_t> &observer) {
+    const int nkf_map = (int)map_keyframes.size();
+    const size_t npt = w.local_pt.size(), n_ept = w.ept_lm.size(), n_eln = w.eln_lm.size();
     std::map<int, KeyFrame *> idx_fix_kfs, idx_nofix_kfs, idx_all_kfs;  // one entry per KF (~100)
     for (auto *k : map_keyframes)  // :5870-5875
         if (k && k->local) {
@@ -373,12 +723,14 @@ int MapHandler::gatherWindow(Window &w) {
             kf_of[o] = idx_all_kfs.at(o);
         }
     w.ept_kfp.resize(n_ept);
+#pragma omp parallel for schedule(static) num_threads(pass_threads(n_ept))
     for (size_t i = 0; i < n_ept; ++i) {
         const int o = w.ept_kf[i];
         w.ept_kf[i] = pos_of[o];
         w.ept_kfp[i] = kf_of[o];
     }
     w.eln_kfp.resize(n_eln);
+#pragma omp parallel for schedule(static) num_threads(pass_threads(n_eln))
     for (size_t i = 0; i < n_eln; ++i) {
         const int o = w.eln_kf[i];
         w.eln_kf[i] = pos_of[o];
@@ -401,7 +753,7 @@ int MapHandler::gatherWindow(Window &w) {
 // any id shared by two vertices of the window: a bitmap over [min, max] when the range is
 // comparable to the vertex count, a sort otherwise
 static bool has_duplicate_id(const Window &w) {
-    const std::vector<int32_t> *lists[3] = {&w.kf_id, &w.pt_id, &w.ln_id};
+    const wvector<int32_t> *lists[3] = {&w.kf_id, &w.pt_id, &w.ln_id};
     size_t n = 0;
     long long lo = 0, hi = -1;
     for (auto *v : lists)
@@ -460,10 +812,21 @@ int MapHandler::solve(const plba_graph &g, plba_result &r) {
             return rc;
         }
     }
+    const auto t0 = std::chrono::steady_clock::now();
     int rc = plba_upload(ctx_, &g);
+    last_upload_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (!rc) rc = plba_lba_plucker(ctx_, &r);
     if (rc) setError("plba: %s", plba_last_error(ctx_));
     return rc;
+}
+
+void MapHandler::storePosition(int kind, int idx, const double *pos) {
+    if (!incremental || !store_->active || idx < 0) return;
+    LmSide &sd = store_->side(kind);
+    if (idx >= (int)sd.e.size()) return;
+    LmEntry &en = sd.e[idx];
+    if (en.dirty || en.off < 0) return;  // (re-read from the object at the next gather anyway)
+    for (int k = 0; k < (kind == 1 ? 3 : 4); ++k) en.pos[k] = pos[k];
 }
 
 // A1d: post-solve outlier bookkeeping (src/mapHandler.cpp:6154-6293), edges in reverse order.
@@ -522,6 +885,7 @@ int MapHandler::outlierPass(Window &w, const std::vector<double> &ept_chi2, cons
                     break;
                 }
             pMP->updateAverageDescDir();
+            markLandmarkChanged(1, lm_idx_map);
             for (int idx : pMP->kf_obs_list)
                 if (kf_obs != idx && !graph_dec(kf_obs, idx)) return PLBA_E_STATE;
         } else {
@@ -546,6 +910,7 @@ int MapHandler::outlierPass(Window &w, const std::vector<double> &ept_chi2, cons
                     break;
                 }
             lML->updateAverageDescDir();
+            markLandmarkChanged(2, lm_idx_map);
             for (int idx : lML->kf_obs_list)
                 if (kf_obs != idx && !graph_dec(kf_obs, idx)) return PLBA_E_STATE;
         } else {
@@ -581,6 +946,8 @@ int MapHandler::localBundleAdjustmentForPlukerWithG2O(LbaStats *stats) {
     rc = solve(g, r);  // A1c (:6119-6152) on the device
     if (rc) return rc;
     const auto t2 = clk::now();
+    st.upload_ms = solve_fn_ ? 0.0 : last_upload_ms_;
+    st.dirty_landmarks = last_dirty_;
     st.iters[0] = r.iters[0]; st.iters[1] = r.iters[1];
     st.chi2[0] = r.chi2[0]; st.chi2[1] = r.chi2[1];
     for (uint8_t l : eln_level) st.bad_line_stage1 += l == 1;  // "Bad Obs" (:6137-6147)
@@ -598,11 +965,20 @@ int MapHandler::localBundleAdjustmentForPlukerWithG2O(LbaStats *stats) {
             for (int b = 0; b < 4; ++b) est[a * 4 + b] = Tcw[k * 12 + a * 4 + b];
         kf->T_kf_w = inverse4(est);
     }
-    for (size_t p = 0; p < w.local_pt.size(); ++p)
+    const size_t nwp = w.local_pt.size(), nwl = w.local_ls.size();
+#pragma omp parallel for schedule(static) num_threads(pass_threads(nwp))
+    for (size_t p = 0; p < nwp; ++p) {
         for (int k = 0; k < 3; ++k) w.local_pt[p]->point3D[k] = xyz[p * 3 + k];
-    for (size_t l = 0; l < w.local_ls.size(); ++l) {
+        storePosition(1, w.local_pt[p]->idx, &xyz[p * 3]);
+    }
+#pragma omp parallel for schedule(static) num_threads(pass_threads(16 * nwl))
+    for (size_t l = 0; l < nwl; ++l) {
         Vec4 o{orth[l * 4], orth[l * 4 + 1], orth[l * 4 + 2], orth[l * 4 + 3]};
         w.local_ls[l]->NDw = MapLine::changeOrthToPluker(o);
+        if (incremental) {  // the next gather's changePlukerToOrth(NDw) (not o: the round trip rounds)
+            const Vec4 o2 = MapLine::changePlukerToOrth(w.local_ls[l]->NDw);
+            storePosition(2, w.local_ls[l]->idx, o2.data());
+        }
     }
     const auto t3 = clk::now();
     st.gather_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -821,6 +1197,7 @@ int MapHandler::localBundleAdjustmentForPluker(HlmStats *stats) {
                 ++st.pt_outliers;
             }
             for (int k = 0; k < 3; ++k) pts[i]->point3D[k] = xyz_out[i * 3 + k];
+            markLandmarkChanged(1, pts[i]->idx);
         }
         for (size_t i = 0; i < lns.size(); ++i) {
             // NDw = changeOrthToPluker(DX) with DX = X − orthNDw: the reference converts the
@@ -836,6 +1213,7 @@ int MapHandler::localBundleAdjustmentForPluker(HlmStats *stats) {
                 ++st.ln_outliers;
             }
             lns[i]->NDw = MapLine::changeOrthToPluker(dx);
+            markLandmarkChanged(2, lns[i]->idx);
         }
         // "Remove bad observations" (:2200-2322) acts on observations flagged -1 in column 5,
         // which nothing sets (:1549, 1591): no-op, as in the reference
@@ -884,18 +1262,53 @@ int MapHandler::formLocalMap(int kf_idx) {
             return PLBA_E_INVALID;
         }
     }
-    // reset local KFs & LMs (:1076-1091)
+    // reset local KFs & LMs (:1076-1091). Incremental: only the registered local landmarks are
+    // reset (the registry holds every landmark whose flag is set), O(window) instead of O(map).
     for (auto *k : map_keyframes)
         if (k) k->local = false;
-    for (auto *p : map_points)
-        if (p) p->local = false;
-    for (auto *l : map_lines)
-        if (l) l->local = false;
+    const bool inc = incremental && store_->active;
+    if (inc) {
+        for (int kind = 1; kind <= 2; ++kind) {
+            LmSide &sd = store_->side(kind);
+            for (int32_t idx : sd.reg) {
+                if (kind == 1 && idx < (int)map_points.size() && map_points[idx]) map_points[idx]->local = false;
+                if (kind == 2 && idx < (int)map_lines.size() && map_lines[idx]) map_lines[idx]->local = false;
+                sd.at(idx).local = 0;
+            }
+            sd.reg.clear();
+            sd.reg_sorted = true;
+        }
+    } else {
+        for (auto *p : map_points)
+            if (p) p->local = false;
+        for (auto *l : map_lines)
+            if (l) l->local = false;
+    }
     auto mark = [&](const KeyFrame *k) {
         for (int lm : k->stereo_frame.stereo_pt_idx)
-            if (lm != -1 && map_points[lm]) map_points[lm]->local = true;
+            if (lm != -1 && map_points[lm]) {
+                map_points[lm]->local = true;
+                if (inc) {
+                    LmEntry &en = store_->pt.at(lm);
+                    if (!en.local) {
+                        en.local = 1;
+                        store_->pt.reg.push_back(lm);
+                        store_->pt.reg_sorted = false;
+                    }
+                }
+            }
         for (int lm : k->stereo_frame.stereo_ls_idx)
-            if (lm != -1 && map_lines[lm]) map_lines[lm]->local = true;
+            if (lm != -1 && map_lines[lm]) {
+                map_lines[lm]->local = true;
+                if (inc) {
+                    LmEntry &en = store_->ln.at(lm);
+                    if (!en.local) {
+                        en.local = 1;
+                        store_->ln.reg.push_back(lm);
+                        store_->ln.reg_sorted = false;
+                    }
+                }
+            }
     };
     // the KF itself and its landmarks (:1094-1113)
     map_keyframes[kf_idx]->local = true;
@@ -963,8 +1376,10 @@ int MapHandler::removeBadMapLandmarksForPluker(CullStats *cs) {
                     break;
                 }
             erase_first(map_points_kf_idx.at(kf_obs), lm_idx);
+            const int slot = (int)(&p - map_points.data());
             delete p;
             p = nullptr;
+            markLandmarkChanged(1, slot);
             st.points_removed++;
         }
     for (auto *&l : map_lines)
@@ -976,8 +1391,10 @@ int MapHandler::removeBadMapLandmarksForPluker(CullStats *cs) {
                     break;
                 }
             erase_first(map_lines_kf_idx.at(kf_obs), lm_idx);
+            const int slot = (int)(&l - map_lines.data());
             delete l;
             l = nullptr;
+            markLandmarkChanged(2, slot);
             st.lines_removed++;
         }
     if (cs) *cs = st;

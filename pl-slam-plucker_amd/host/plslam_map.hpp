@@ -11,12 +11,40 @@
 #include <array>
 #include <cstdint>
 #include <map>
+#include <memory>
+#include <new>
+#include <utility>
 #include <string>
 #include <vector>
 
 #include "plba.h"
 
 namespace plslam {
+
+// Incremental window state of a MapHandler (map_handler.cpp): landmarks report changes to it.
+struct LandmarkStore;
+void landmark_changed(LandmarkStore *s, int kind, int idx);  // kind 1 = point, 2 = line
+
+// The marshalled window's arrays: resize() default-initialises (no zero fill) — every element
+// is written by the gather. (Page-locked memory for them was measured and did not shorten
+// plba_upload: 0.97 vs 0.92-0.96 ms at C3.)
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U> &) {}
+    template <class U, class... Args>
+    void construct(U *p, Args &&...args) {
+        if constexpr (sizeof...(Args) == 0) ::new ((void *)p) U;
+        else ::new ((void *)p) U(std::forward<Args>(args)...);
+    }
+};
+template <class T>
+using wvector = std::vector<T, DefaultInitAlloc<T>>;
 
 using Vec2 = std::array<double, 2>;
 using Vec3 = std::array<double, 3>;
@@ -56,6 +84,7 @@ struct MapPoint {
     std::vector<Vec3> dir_list;
     std::vector<int> kf_obs_list;
     std::vector<double> sigma_list;
+    LandmarkStore *store = nullptr;  // the owning MapHandler's incremental window (set when placed)
 
     MapPoint(int idx_, const Vec3 &p, const Desc &desc, int kf_obs, const Vec2 &obs, const Vec3 &dir, double sigma2);
     void addMapPointObservation(const Desc &desc, int kf_obs, const Vec2 &obs, const Vec3 &dir, double sigma2);
@@ -81,6 +110,7 @@ struct MapLine {
     Vec6 line3D{};
     Vec3 med_obs_dir{};
     std::vector<Vec3> dir_list;
+    LandmarkStore *store = nullptr;
 
     MapLine(int idx_, const Vec6 &NDw_, const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2);
     void addMapLineObservation(const Desc &desc, int kf_obs, const Vec4 &obs, double sigma2);
@@ -98,9 +128,9 @@ struct Window {
     std::vector<MapLine *> local_ls;
     int max_kf_id = 0, maxPointId = 0;
     // plba_graph arrays
-    std::vector<double> kf_Tcw, pt_xyz, ln_orth, ept_obs, ept_info, eln_obs, eln_info;
-    std::vector<uint8_t> kf_fixed;
-    std::vector<int32_t> kf_id, pt_id, ln_id, ept_lm, ept_kf, eln_lm, eln_kf;
+    wvector<double> kf_Tcw, pt_xyz, ln_orth, ept_obs, ept_info, eln_obs, eln_info;
+    wvector<uint8_t> kf_fixed;
+    wvector<int32_t> kf_id, pt_id, ln_id, ept_lm, ept_kf, eln_lm, eln_kf;
     // per-edge back references
     std::vector<KeyFrame *> ept_kfp, eln_kfp;
     std::vector<int> ept_obs_idx, eln_obs_idx;
@@ -117,6 +147,8 @@ struct LbaStats {
     int iters[2] = {0, 0};
     double chi2[2] = {0, 0};
     double gather_ms = 0, solve_ms = 0, bookkeeping_ms = 0;
+    double upload_ms = 0;      // plba_upload, part of solve_ms
+    int dirty_landmarks = 0;   // landmarks re-read from their objects by the gather (incremental mode)
 };
 
 using SolveFn = int (*)(void *user, const plba_graph *g, plba_result *r);
@@ -215,7 +247,30 @@ class MapHandler {
     // window gather + marshalling (A1, A1b) — public for tests
     int gatherWindow(Window &w);
 
+    // ---- incremental window (round 6). The handler keeps every landmark's
+    // observations flattened into arenas and the set of local landmarks as a registry, so that the
+    // gather and formLocalMap cost O(window + changes), not O(map): the reference scans every map
+    // landmark (src/mapHandler.cpp:5877-5886, :1076-1091). Landmarks report changes through
+    // landmark_changed: placed / replaced (adoptLandmark), observations added (their methods),
+    // erased by the outlier pass, deleted by the culling, moved by the loop closure or the hand-rolled
+    // LBA. A caller that writes a landmark's fields directly calls markLandmarkChanged, or
+    // rebuildLocalRegistry after writing `local` flags, or sets incremental = false (the scan gather).
+    bool incremental = true;
+    void adoptLandmark(int kind, int idx);
+    void markLandmarkChanged(int kind, int idx);
+    int setLandmarkLocal(int kind, int idx, bool local);
+    void rebuildLocalRegistry();
+    // tests: the landmark pass of both gathers on the current map, compared (0 = equal); no mutation
+    int checkIncrementalGather(std::string *why = nullptr);
+
   private:
+    int gatherScan(Window &w, std::vector<uint8_t> &observer);
+    int gatherIncremental(Window &w, std::vector<uint8_t> &observer, int *dirty);
+    int finishGather(Window &w, const std::vector<uint8_t> &observer);
+    std::unique_ptr<LandmarkStore> store_;
+    int last_dirty_ = 0;
+    double last_upload_ms_ = 0;
+    void storePosition(int kind, int idx, const double *pos);  // write-back: the cached position
     int solve(const plba_graph &g, plba_result &r);
     int ensureCtx();
     int outlierPass(Window &w, const std::vector<double> &ept_chi2, const std::vector<uint8_t> &ept_depth_ok,

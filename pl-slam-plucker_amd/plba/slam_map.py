@@ -176,7 +176,8 @@ class PlslamLbaStats(C.Structure):
                 ("bad_point_obs", C.c_int32), ("actually_bad_point_obs", C.c_int32),
                 ("bad_line_obs", C.c_int32), ("actually_bad_line_obs", C.c_int32),
                 ("iters", C.c_int32 * 2), ("chi2", C.c_double * 2),
-                ("gather_ms", C.c_double), ("solve_ms", C.c_double), ("bookkeeping_ms", C.c_double)]
+                ("gather_ms", C.c_double), ("solve_ms", C.c_double), ("bookkeeping_ms", C.c_double),
+                ("upload_ms", C.c_double), ("dirty_landmarks", C.c_int32)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
@@ -227,6 +228,7 @@ HOST_EXPORTED = [
     "plslam_local_ba_plucker",
     "plslam_set_loop_closure", "plslam_get_lc_idx_list", "plslam_set_pgo_params", "plslam_set_pgo_solver",
     "plslam_loop_closure_optimization", "plslam_set_line_geometry", "plslam_get_line_geometry",
+    "plslam_set_incremental", "plslam_mark_landmark_changed", "plslam_check_incremental_gather",
 ]
 
 
@@ -295,6 +297,9 @@ def load_host(path: Optional[str] = None):
     L.plslam_loop_closure_optimization.argtypes = [vp, C.c_int32, C.POINTER(PlslamPgoStats)]
     L.plslam_set_line_geometry.argtypes = [vp, C.c_int32, dp, dp]
     L.plslam_get_line_geometry.argtypes = [vp, C.c_int32, dp, dp]
+    L.plslam_set_incremental.argtypes = [vp, C.c_int32]
+    L.plslam_mark_landmark_changed.argtypes = [vp, C.c_int32, C.c_int32]
+    L.plslam_check_incremental_gather.argtypes = [vp, ip]
     for n in HOST_EXPORTED:
         if n not in ("plslam_map_last_error", "plslam_pluker_to_orth", "plslam_orth_to_pluker"):
             getattr(L, n).restype = C.c_int
@@ -395,6 +400,49 @@ class HostMap:
             self._check(L.plslam_kf_lines_idx_set(h, k, a.ctypes.data_as(ip), len(a)), "kf_lines_idx_set")
         self._check(L.plslam_set_max_kf_idx(h, int(m.max_kf_idx)), "max_kf_idx")
 
+    def add_background(self, n_kf: int, n_pt: int, n_ln: int, seed: int = 0, obs_per_lm=(2, 5)):
+        """Non-local keyframes and landmarks around the window (appended after the existing slots):
+        e.g. a C5-sized map (BASELINE.json configs[4]: 1000 KF / 200k points / 40k lines) holding a
+        C3 window, so that the per-call cost of the LBA is measured on a map of real size. Each
+        background landmark is observed by 2-4 of the new keyframes; none is local."""
+        L, h = self.L, self.h
+        rng = np.random.default_rng(seed)
+        ip, dp = C.POINTER(C.c_int32), C.POINTER(C.c_double)
+        k0 = self.n_kf
+        for k in range(n_kf):
+            T = np.eye(4)
+            T[:3, 3] = rng.normal(size=3) * 10
+            Tc = np.ascontiguousarray(T.reshape(16))
+            self._check(L.plslam_add_keyframe(h, k0 + k, Tc.ctypes.data_as(dp), 0, None, 0, None), "add_keyframe")
+        self.n_kf += n_kf
+        for kind, n, width in ((1, n_pt, 2), (2, n_ln, 4)):
+            base = self.n_pt if kind == 1 else self.n_ln
+            nobs = rng.integers(obs_per_lm[0], obs_per_lm[1], size=n)
+            kfs = (k0 + rng.integers(0, max(n_kf, 1), size=int(nobs.sum()))).astype(np.int32)
+            obs = np.ascontiguousarray(rng.uniform(0, 700, size=(int(nobs.sum()), width)))
+            pos = np.ascontiguousarray(rng.normal(size=(n, 3 if kind == 1 else 6)) * 5)
+            d3 = np.ascontiguousarray(np.array([0.0, 0.0, 1.0]))
+            po, oo, dd = pos.ctypes.data, obs.ctypes.data, d3.ctypes.data_as(dp)
+            e = 0
+            for i in range(n):
+                idx = base + i
+                xp = C.cast(po + i * pos.shape[1] * 8, dp)
+                for j in range(int(nobs[i])):
+                    op = C.cast(oo + e * width * 8, dp)
+                    if j == 0:
+                        rc = (L.plslam_add_point(h, idx, xp, None, DESC_BYTES, int(kfs[e]), op, dd, 1.0) if kind == 1
+                              else L.plslam_add_line(h, idx, xp, None, DESC_BYTES, int(kfs[e]), op, 1.0))
+                    else:
+                        rc = (L.plslam_point_add_observation(h, idx, None, int(kfs[e]), op, dd, 1.0) if kind == 1
+                              else L.plslam_line_add_observation(h, idx, None, int(kfs[e]), op, 1.0))
+                    if rc:
+                        self._check(rc, "add background landmark")
+                    e += 1
+            if kind == 1:
+                self.n_pt += n
+            else:
+                self.n_ln += n
+
     def set_solver(self, fn: Optional[Callable]):
         """fn(graph: PlbaGraph, result: PlbaResult) -> int, or None for the MI355X backend."""
         if fn is None:
@@ -412,6 +460,19 @@ class HostMap:
                 return -1
         self._cb = SOLVE_FN(tramp)
         self._check(self.L.plslam_set_solver(self.h, self._cb, None), "set_solver")
+
+    def set_incremental(self, on: bool):
+        self._check(self.L.plslam_set_incremental(self.h, int(on)), "set_incremental")
+
+    def mark_landmark_changed(self, kind: int, idx: int):
+        self._check(self.L.plslam_mark_landmark_changed(self.h, kind, idx), "mark_landmark_changed")
+
+    def check_incremental_gather(self) -> bool:
+        e = C.c_int32()
+        self._check(self.L.plslam_check_incremental_gather(self.h, C.byref(e)), "check_incremental_gather")
+        if not e.value:
+            self._why = self.L.plslam_map_last_error(self.h).decode(errors="replace")
+        return bool(e.value)
 
     def local_ba(self) -> dict:
         st = PlslamLbaStats()

@@ -340,3 +340,80 @@ def test_gpu_local_mapping_step_matches_model_with_oracle():
               "bad_line_obs", "actually_bad_line_obs", "iters", "points_removed", "lines_removed"):
         assert st[k] == st_model[k], (k, st[k], st_model[k])
     hm.compare_maps(hmap.read(m), want, pose_tol=1e-4, lm_tol=1e-4)
+
+
+# ---- incremental window (round 6)
+def _mapping_sequence(hmap, m, rng):
+    """A few local-mapping steps with map edits in between: new observations through the C ABI,
+    local flags set and cleared, and the LBA's own outlier pass / write-back / culling."""
+    L, h = hmap.L, hmap.h
+    seq = [len(m.keyframes) - 1, len(m.keyframes) - 3, len(m.keyframes) - 2]
+    for step, kf_idx in enumerate(seq):
+        yield f"step{step}:before"
+        hmap.local_mapping_step(kf_idx)
+        yield f"step{step}:after"
+        # a new observation of a few live points and lines (addMapPointObservation / addMapLineObservation)
+        live_pt = [i for i in range(hmap.n_pt) if hmap.exists(1, i)]
+        for idx in rng.choice(live_pt, size=3, replace=False):
+            o = np.array([100.0 + idx, 50.0 + step])
+            d = np.array([0.0, 0.0, 1.0])
+            desc = np.zeros(32, np.uint8)
+            assert L.plslam_point_add_observation(h, int(idx), desc.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                  int(kf_idx), o.ctypes.data_as(C.POINTER(C.c_double)),
+                                                  d.ctypes.data_as(C.POINTER(C.c_double)), 1.3) == 0
+        live_ln = [i for i in range(hmap.n_ln) if hmap.exists(2, i)]
+        if live_ln:
+            idx = int(rng.choice(live_ln))
+            o = np.array([10.0, 20.0, 300.0, 40.0 + step])
+            desc = np.zeros(32, np.uint8)
+            assert L.plslam_line_add_observation(h, idx, desc.ctypes.data_as(C.POINTER(C.c_uint8)), int(kf_idx),
+                                                 o.ctypes.data_as(C.POINTER(C.c_double)), 0.7) == 0
+        yield f"step{step}:observations"
+        # local flags written through the ABI (the registry follows them)
+        for idx in rng.choice(live_pt, size=4, replace=False):
+            assert L.plslam_set_local(h, 1, int(idx), int(rng.random() < 0.5)) == 0
+        yield f"step{step}:flags"
+
+
+@pytest.mark.parametrize("cfg,seed", [("C1L", 31), ("C2", 32)])
+def test_incremental_gather_equals_the_scan_gather(cfg, seed):
+    """The registry + cached-run gather hands the solver exactly what the reference's map scan
+    would, after every kind of map change the local-mapping loop makes."""
+    m = _aged(make_map(synth.generate(cfg, fixed_frac=0.3), seed=seed, n_extra_pt=40), extra=5)
+    hmap, _ = host_with(m, stub_solve)
+    p = _step_params(m, len(m.keyframes) - 1)
+    hmap.L.plslam_set_params(hmap.h, p.min_lm_obs, p.min_lm_cov_graph, p.min_kf_local_map)
+    assert hmap.check_incremental_gather()
+    for tag in _mapping_sequence(hmap, m, np.random.default_rng(seed)):
+        assert hmap.check_incremental_gather(), (tag, getattr(hmap, "_why", ""))
+
+
+def test_incremental_and_scan_modes_leave_the_same_map():
+    """The same local-mapping sequence on two handlers, one gathering incrementally (default) and
+    one scanning the map as the reference: identical marshalled windows, statistics and maps."""
+    m = _aged(make_map(synth.generate("C1L", fixed_frac=0.3), seed=33, n_extra_pt=40), extra=5)
+    p = _step_params(m, len(m.keyframes) - 1)
+    runs = []
+    for inc in (True, False):
+        hmap, seen = host_with(m, stub_solve)
+        hmap.set_incremental(inc)
+        hmap.L.plslam_set_params(hmap.h, p.min_lm_obs, p.min_lm_cov_graph, p.min_kf_local_map)
+        graphs, stats = [], []
+        orig = hmap._cb
+
+        for tag in _mapping_sequence(hmap, m, np.random.default_rng(33)):
+            if tag.endswith(":after"):
+                graphs.append(seen["graph"])
+        st = hmap.local_ba()
+        stats.append({k: v for k, v in st.items() if not k.endswith("_ms") and k != "dirty_landmarks"})
+        graphs.append(seen["graph"])
+        runs.append((graphs, stats, hmap.read(m), st["dirty_landmarks"]))
+        assert orig is hmap._cb
+    (ga, sa, ma, da), (gb, sb, mb, db) = runs
+    assert sa == sb
+    for a, b in zip(ga, gb):
+        for f in ("kf_Tcw", "kf_fixed", "kf_id", "pt_xyz", "pt_id", "ln_orth", "ln_id", "ept_lm", "ept_kf", "ept_obs",
+                  "ept_info", "eln_lm", "eln_kf", "eln_obs", "eln_info"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    hm.compare_maps(ma, mb, pose_tol=0, lm_tol=0)
+    assert db == 0 and 0 < da < ga[-1].n_pt + ga[-1].n_ln   # the repeat call re-read only the changed landmarks
