@@ -462,7 +462,7 @@ inline hipError_t launch_band(Dev &d, hipStream_t s) {
     void *args[] = {&d};
     if (d.bcr) {  // forward elimination, then back substitution + pose update (plba_bcr.hpp)
         hipError_t e = hipLaunchKernel(bcr_kernel(d.bw), dim3(d.bcr_N, d.spec_max), dim3(kBcrNT), args, bcr_lds_bytes(d.bw), s);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess || d.bcr_fused) return e;
         return hipLaunchKernel(bcr_back_kernel(d.bw), dim3(d.bcr_N, d.spec_max), dim3(kBcrBackNT), args,
                                bcr_back_lds_bytes(d.bw), s);
     }
@@ -1038,6 +1038,8 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
     const bool bcr = band_mode && !ctx->no_bcr && want_bcr(bw, nf, bcr_res);
     d.bcr = bcr ? 1 : 0;
     d.bcr_N = bcr ? (nf + bw - 1) / bw : 0;
+    // BCR back substitution inside the forward launch (PLBA_BCR_SPLIT=1: the second launch)
+    d.bcr_fused = bcr && !env_flag("PLBA_BCR_SPLIT") ? 1 : 0;
     const bool cl = band_mode && !bcr && use_cl(bw);
     const bool twisted = band_mode && !bcr && bw >= 1 && nf >= 2 * bw + 16 &&
                          (cl ? cl_lds_bytes(bw, nf, true) : twisted_lds_bytes(bw, nf) + band_static_bytes(bw)) <= 159 * 1024 &&
@@ -1561,7 +1563,7 @@ int graph_levels() {  // (read per capture: tests switch it)
 std::vector<int64_t> launch_signature(const plba_ctx *ctx) {
     const Dev &d = ctx->d;
     return {d.E > 0, d.nf > 0, d.n_lm > 0, d.n > 0, d.nch > 0, d.band_mode, d.dense_mfma, d.dense_mfma ? d.ntiles : 0,
-            d.bw, d.bcr, d.cl, d.twisted, d.sharded, d.xg_P, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
+            d.bw, d.bcr, d.bcr_fused, d.cl, d.twisted, d.sharded, d.xg_P, d.fold, d.fold_init, d.n_kf > 0, d.spec_max,
             (int64_t)(getenv("PLBA_CHUNK_DIRECT") != nullptr), (int64_t)chunk_half(d), (int64_t)ctx->comm.kind};
 }
 int capture_step(plba_ctx *ctx) {

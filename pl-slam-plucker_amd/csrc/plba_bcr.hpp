@@ -567,18 +567,133 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d0) {
             __syncthreads();
         }
         BCR_STAMP(14);
-        // ---- X = D_m⁻¹ [U | V | b] for the backward kernel; the root holds the solution x_0 itself
+        // ---- X = D_m⁻¹ [U | V | b] for the backward kernel (split mode); the root holds the solution
+        //      x_0 itself. Fused mode (default): X stays in Rm and this workgroup back-substitutes its
+        //      own super-row below, so X never goes through memory and the second launch is gone.
+        const bool fused = d.bcr_fused != 0;
+        const int XR = bcr_xrec(BW);
         if (!root) {
-            double *Xg = d.bcr_X + (size_t)m * S * NX;
-            for (int t = tid; t < S * NX; t += NT) Xg[t] = Rm[(t / NX) * RS + t % NX];
+            if (!fused) {
+                double *Xg = d.bcr_X + (size_t)m * S * NX;
+                for (int t = tid; t < S * NX; t += NT) Xg[t] = Rm[(t / NX) * RS + t % NX];
+            }
         } else {
             for (int r = tid; r < S; r += NT) st_sc1(d.bcr_x + r, Rm[r * RS + 2 * S]);
             // every failure word has flowed in (PLBA_DIAG bit 128: the tests' forced failures)
-            if (tid == 0) *d.solve_okp = (fail_fwd != 0.0 || diag_fail(d)) ? 0 : 1;
+            if (tid == 0) {
+                const bool failed0 = fail_fwd != 0.0 || diag_fail(d);
+                *d.solve_okp = failed0 ? 0 : 1;
+                // fused: the decision travels down the tree in the x records (slot S), so every
+                // row's pose update knows it without reading solve_ok across workgroups
+                st_sc1(d.bcr_x + S, failed0 ? 1.0 : 0.0);
+            }
             bcr_publish(&d.bcr_flag[1], epoch);
         }
         BCR_STAMP(16);
-        // ---- arrival: the last workgroup resets the ticket counter for the next launch
+        if (fused) {
+            // ---- back substitution of this super-row: x_m = X_b - X_U x_a - X_V x_c once the
+            //      neighbours (higher levels: later tickets, co-resident by the selection rule — a
+            //      timed-out wait raises Ctrl::dev_error and the host re-solves) are solved; then
+            //      the pose update of its poses (as k_rcs_bcr_back).
+            constexpr int NPART = NT / S < kBcrParts ? NT / S : kBcrParts;
+            double *xa = xv, *xc = xv + S, *xm = xv + 2 * S, *red = pv + 96, *ps = red + kBcrParts * S;
+            __shared__ double s_sum[NT / 64];
+            __shared__ double s_failed;
+            __shared__ int s_kf[BW + 1];
+            const int a_row = m - (1 << lm), c_row = m + (1 << lm);
+            const double *Tc0 = d.Tc;
+            double *Tt0 = d.Tt;
+            if (tid < BW) s_kf[tid] = m * BW + tid < nf ? d.h_kf[m * BW + tid] : 0;
+            for (int t = tid; t < BW * 24; t += NT) {
+                const int i = t / 24, q = t % 24, h = m * BW + i;
+                double v = 0.0;
+                if (h < nf) {
+                    const int kf = d.h_kf[h];
+                    v = q < 12 ? Tc0[(size_t)kf * 12 + q] : (q < 18 ? d.bp[(size_t)h * 6 + q - 12] : d.xp_prev[(size_t)h * 6 + q - 18]);
+                }
+                ps[t] = v;
+            }
+            const bool hlm0 = d.ctrl->hlm != 0;
+            for (int k = m + N * tid; k < d.n_kf; k += N * NT)
+                if (d.kf_hidx[k] < 0) {
+#pragma unroll
+                    for (int q = 0; q < 12; ++q) Tt0[(size_t)k * 12 + q] = Tc0[(size_t)k * 12 + q];
+                    if (hlm0)
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) d.xkt[(size_t)k * 6 + q] = d.xkc[(size_t)k * 6 + q];
+                }
+            if (!root) {
+                if (tid == 0) (void)bcr_poll(&d.bcr_flag[2 * a_row + 1], epoch, &d.ctrl->dev_error, d.diag);
+                if (hasC && tid == 64) (void)bcr_poll(&d.bcr_flag[2 * c_row + 1], epoch, &d.ctrl->dev_error, d.diag);
+                __syncthreads();
+                for (int t = tid; t < S; t += NT) {
+                    xa[t] = ld_sc1(d.bcr_x + (size_t)a_row * XR + t);
+                    xc[t] = hasC ? ld_sc1(d.bcr_x + (size_t)c_row * XR + t) : 0.0;
+                }
+                if (tid == 0) s_failed = ld_sc1(d.bcr_x + (size_t)a_row * XR + S);
+                __syncthreads();
+                if (tid < S * NPART) {  // mat-vec in column slices per row, partials summed in slice order
+                    const int r = tid % S, part = tid / S;
+                    constexpr int CPP = (2 * S + NPART - 1) / NPART;
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int u = 0; u < CPP; ++u) {
+                        const int q = part * CPP + u;
+                        if (q < S) sacc = fma(Rm[r * RS + q], xa[q], sacc);
+                        else if (q < 2 * S && hasC) sacc = fma(Rm[r * RS + q], xc[q - S], sacc);
+                    }
+                    red[part * S + r] = sacc;
+                }
+                __syncthreads();
+                for (int r = tid; r < S; r += NT) {
+                    double sacc = Rm[r * RS + 2 * S];
+                    for (int part = 0; part < NPART; ++part) sacc -= red[part * S + r];
+                    xm[r] = sacc;
+                    st_sc1(d.bcr_x + (size_t)m * XR + r, sacc);
+                }
+                if (tid == 0) st_sc1(d.bcr_x + (size_t)m * XR + S, s_failed);
+                bcr_publish(&d.bcr_flag[2 * m + 1], epoch);
+            } else {
+                for (int r = tid; r < S; r += NT) xm[r] = Rm[r * RS + 2 * S];
+                if (tid == 0) s_failed = (fail_fwd != 0.0 || diag_fail(d)) ? 1.0 : 0.0;
+                __syncthreads();
+            }
+            // ---- this super-row's poses: x_p (kept from the previous trial if the solve failed, A13),
+            //      oplus into the trial state, pose part of Σx(λx+b)
+            const bool failed = s_failed != 0.0;
+            const double lam = d.lam;
+            double sc = 0.0;
+            if (tid < BW) {
+                const int h = m * BW + tid;
+                if (h < nf) {
+                    const double *pp = ps + tid * 24;
+                    double x[6];
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) x[q] = failed ? pp[18 + q] : xm[6 * tid + q];
+                    if (!failed)
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) d.xp[6 * h + q] = x[q];
+                    if (hlm0) {  // hand-rolled LM: se(3) update, ‖DX‖² part
+                        const int kf = s_kf[tid];
+                        double xn[6];
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) sc += x[q] * x[q];
+                        hlm_pose_update(d.xkc + (size_t)kf * 6, x, xn, Tt0 + (size_t)kf * 12);
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) d.xkt[(size_t)kf * 6 + q] = xn[q];
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) sc += x[q] * (lam * x[q] + pp[12 + q]);
+                        pose_oplus(pp, x, Tt0 + (size_t)s_kf[tid] * 12);
+                    }
+                }
+            }
+            const double ssum = block_sum<NT>(sc, s_sum);
+            if (tid == 0) d.part_ps[m] = ssum;
+        }
+        BCR_STAMP(18);
+        // ---- arrival: the last workgroup resets the ticket counter for the next launch (fused: and
+        //      advances the epoch, as the backward launch's last workgroup does in split mode)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
@@ -586,6 +701,7 @@ __global__ __launch_bounds__(kBcrNT) void k_rcs_factor_bcr(Dev d0) {
             if (old == (uint32_t)(N - 1)) {
                 __hip_atomic_store(&d.bcr_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&d.bcr_ctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (fused) __hip_atomic_store(&d.bcr_ctl[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         BCR_STAMP(17);

@@ -210,6 +210,8 @@ struct Dev {
     int32_t *tw_fail, *tw_count;        // [2] per-segment failure, arrival counter
     // block cyclic reduction over super-rows of bw pose blocks (plba_bcr.hpp)
     int32_t bcr, bcr_N;                 // enabled; super-rows (= workgroups of the launch)
+    int32_t bcr_fused;                  // back substitution + pose update in the forward launch (1) or
+                                        // a second launch, k_rcs_bcr_back (0: PLBA_BCR_SPLIT=1)
     double *bcr_pub;                    // [N][bcr_pub_doubles(bw)] Schur contributions + coupling
     double *bcr_x;                      // [N][6 bw] solution of each super-row
     double *bcr_X;                      // [N][6 bw][12 bw + 1] X = D_m⁻¹[U | V | b] (forward -> backward)

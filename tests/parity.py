@@ -71,3 +71,19 @@ def compare(gpu: dict, ref: dict, rtol=EST_RTOL):
         pt_bad_diff=int(((gpu["ept_chi2"] > 5.991) | (gpu["ept_depth_ok"] == 0)).astype(int).sum()
                         - ((ref["ept_chi2"] > 5.991) | (ref["ept_depth_ok"] == 0)).astype(int).sum()),
     )
+
+
+def assert_trace_parity(out: dict, ref: dict, rtol=1e-6):
+    """The per-iteration trace of BOTH stages: same stage / iteration, the same
+    trial count and result while the iteration still makes progress, χ² at linearisation and after
+    the trial loop within rtol. (Damped-trial counts are decided by the sign of ρ; once an
+    iteration's χ² decrease is at rounding level — converged — that sign is noise on either side.)"""
+    tg, tr = out["trace"], ref["trace"]
+    assert len(tg) == len(tr) == int(sum(max(i, 0) for i in ref["iters"])), (len(tg), len(tr))
+    for i in range(len(tr)):
+        for k in ("stage", "iter"):
+            assert tg[i][k] == tr[i][k], (i, k, tg[i], tr[i])
+        if tr[i]["chi2_start"] - tr[i]["chi2_end"] > 1e-9 * tr[i]["chi2_start"]:
+            assert tg[i]["trials"] == tr[i]["trials"] and tg[i]["result"] == tr[i]["result"], (i, tg[i], tr[i])
+        for k in ("chi2_start", "chi2_end"):
+            assert abs(tg[i][k] - tr[i][k]) <= rtol * abs(tr[i][k]), (i, k, tg[i], tr[i])
