@@ -338,7 +338,9 @@ inline int band_ring(int bw, int nf) {
 }
 inline size_t band_lds_bytes(int bw, int nf) { return sizeof(double) * band_lds_doubles(bw, band_ring(bw, nf)); }
 inline size_t twisted_lds_bytes(int bw, int nf) {
-    return std::max(band_lds_bytes(bw, nf), sizeof(double) * (twisted_merge_doubles(bw) + (size_t)nf * 6));  // + x_p staging
+    // x_p staging [nf][6], then the separator merge or (bw >= 11) the streamed back substitution
+    const size_t tail = std::max(twisted_merge_doubles(bw), bw * 6 > 64 ? bstream_doubles(bw) : (size_t)0);
+    return std::max(band_lds_bytes(bw, nf), sizeof(double) * ((size_t)nf * 6 + tail));
 }
 template <int... B>
 const void *cl_kernel_impl(int bw, bool twisted, std::integer_sequence<int, B...>) {

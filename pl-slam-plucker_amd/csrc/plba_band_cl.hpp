@@ -38,47 +38,7 @@ __host__ __device__ constexpr size_t cl_lds_doubles(int bw) {
            2 * ((size_t)(bw + 1) * 36 + 6);
 }
 
-// v_rcp_f64 + one Newton step (the estimate is good to ~2^-26, one step squares the error)
-__device__ __forceinline__ double rcp_nr1(double x) {
-    const double r = __builtin_amdgcn_rcp(x);
-    return fma(fma(-x, r, 1.0), r, r);
-}
-
-// Lane-local LDLᵀ of a 6x6 symmetric block held as its packed lower triangle (row-major,
-// ltri(i, j) for j <= i): on return s holds the unit lower factor below the diagonal and dv the
-// reciprocal pivots. zp is set if a pivot is exactly zero (SimplicialLDLT's failure condition).
-__host__ __device__ constexpr int ltri(int i, int j) { return i * (i + 1) / 2 + j; }
-__device__ __forceinline__ void ldl6_inplace(double (&s)[21], double (&dv)[6], bool &zp) {
-#pragma unroll
-    for (int p = 0; p < 6; ++p) {
-        const double dp = s[ltri(p, p)];
-        zp = zp || dp == 0.0;
-        const double rp = rcp_nr1(dp);
-        dv[p] = rp;
-        double col[6];
-#pragma unroll
-        for (int i = p + 1; i < 6; ++i) col[i] = s[ltri(i, p)];
-#pragma unroll
-        for (int i = p + 1; i < 6; ++i) s[ltri(i, p)] = col[i] * rp;
-#pragma unroll
-        for (int i = p + 1; i < 6; ++i)
-#pragma unroll
-            for (int j = p + 1; j <= i; ++j) s[ltri(i, j)] = fma(-s[ltri(i, p)], col[j], s[ltri(i, j)]);
-    }
-}
-// x <- (L D Lᵀ)⁻¹ x with the factors of ldl6_inplace
-__device__ __forceinline__ void ldl6_solve(const double (&s)[21], const double (&dv)[6], double (&x)[6]) {
-#pragma unroll
-    for (int i = 1; i < 6; ++i)
-#pragma unroll
-        for (int m = 0; m < i; ++m) x[i] = fma(-s[ltri(i, m)], x[m], x[i]);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) x[i] *= dv[i];
-#pragma unroll
-    for (int i = 4; i >= 0; --i)
-#pragma unroll
-        for (int m = 5; m > i; --m) x[i] = fma(-s[ltri(m, i)], x[m], x[i]);
-}
+// (rcp_nr1, ltri, ldl6_inplace, ldl6_solve: plba_kernels.hpp, shared with the register-window band kernel)
 
 // Eliminates block rows k0..k1-1 of an nrows-row band (g.nrows). The LDS window (row i in slot
 // i mod (bw+2), block (i, i-w) row-major) is loaded for rows k0..k0+bw+1 when load_window is

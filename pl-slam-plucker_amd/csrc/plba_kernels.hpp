@@ -1735,6 +1735,75 @@ __device__ __forceinline__ double rcp_nr(double x) {
     r = fma(fma(-x, r, 1.0), r, r);
     return r;
 }
+// v_rcp_f64 + one Newton step (the estimate is good to ~2^-26, one step squares the error)
+__device__ __forceinline__ double rcp_nr1(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return fma(fma(-x, r, 1.0), r, r);
+}
+
+// Lane-local LDLᵀ of a 6x6 symmetric block held as its packed lower triangle (row-major,
+// ltri(i, j) for j <= i): on return s holds the unit lower factor below the diagonal and dv the
+// reciprocal pivots. zp is set if a pivot is exactly zero (SimplicialLDLT's failure condition).
+__host__ __device__ constexpr int ltri(int i, int j) { return i * (i + 1) / 2 + j; }
+__device__ __forceinline__ void ldl6_inplace(double (&s)[21], double (&dv)[6], bool &zp) {
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+        const double dp = s[ltri(p, p)];
+        zp = zp || dp == 0.0;
+        const double rp = rcp_nr1(dp);
+        dv[p] = rp;
+        double col[6];
+#pragma unroll
+        for (int i = p + 1; i < 6; ++i) col[i] = s[ltri(i, p)];
+#pragma unroll
+        for (int i = p + 1; i < 6; ++i) s[ltri(i, p)] = col[i] * rp;
+#pragma unroll
+        for (int i = p + 1; i < 6; ++i)
+#pragma unroll
+            for (int j = p + 1; j <= i; ++j) s[ltri(i, j)] = fma(-s[ltri(i, p)], col[j], s[ltri(i, j)]);
+    }
+}
+// x <- (L D Lᵀ)⁻¹ x with the factors of ldl6_inplace
+__device__ __forceinline__ void ldl6_solve(const double (&s)[21], const double (&dv)[6], double (&x)[6]) {
+#pragma unroll
+    for (int i = 1; i < 6; ++i)
+#pragma unroll
+        for (int m = 0; m < i; ++m) x[i] = fma(-s[ltri(i, m)], x[m], x[i]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] *= dv[i];
+#pragma unroll
+    for (int i = 4; i >= 0; --i)
+#pragma unroll
+        for (int m = 5; m > i; --m) x[i] = fma(-s[ltri(m, i)], x[m], x[i]);
+}
+
+// Lane-local inverse of a 6x6 pivot block just published to LDS (entry (r, c) at S[r * 6 + c]; its
+// lower triangle is read): every lane factors S LDLᵀ in its own registers, then lanes r*6+c
+// (0..35) return (S⁻¹)[r][c] (column c of S⁻¹ solved from e_c) and lanes 36+r return (S⁻¹y)[r].
+// No cross-lane traffic: replaces gj_inverse6's 6 pivot broadcasts + 18 LDS permutes, which on
+// the register-window band kernel contend with the worker waves' trailing-update LDS reads.
+// The LDLᵀ pivots are the system's, so a zero pivot fails the solve as SimplicialLDLT does.
+// (LDS operations of one wave complete in order: the caller's stores of S and y need no wait.)
+__device__ __forceinline__ double ldl_inverse6(const double *S, const double *y, int lane, bool &fail) {
+    double s[21], dv[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) s[ltri(i, j)] = S[i * 6 + j];
+    bool zp = false;
+    ldl6_inplace(s, dv, zp);
+    if (zp) fail = true;
+    const bool mat = lane < 36;
+    const int r = mat ? lane / 6 : min(lane - 36, 5), c = lane % 6;
+    double x[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) x[m] = mat ? (m == c ? 1.0 : 0.0) : y[m];
+    ldl6_solve(s, dv, x);
+    double out = x[0];
+#pragma unroll
+    for (int m = 1; m < 6; ++m) out = r == m ? x[m] : out;
+    return out;
+}
 // Gauss–Jordan on [S | y] (6x7, one entry per lane): lanes r*6+c (0..35) hold S and return
 // S^{-1}; lanes 36+r hold y and return z = S^{-1} y. No pivoting: the pivots are the LDLᵀ
 // pivots, so a zero pivot reports failure exactly as SimplicialLDLT's NumericalIssue does.
@@ -1823,11 +1892,12 @@ __host__ __device__ constexpr size_t band_lds_doubles(int bw, int R) {
 // ds_read after such a load waits for it)
 __host__ __device__ constexpr size_t band_static_bytes(int bw) { return 16 * ((size_t)(bw + 1) * 36 + 6) + 64; }
 // The twisted kernel's merge, after both segments have exported their separator windows, reuses
-// the LDS from 0: the separator system's packed lower triangle [6bw(6bw+1)/2], its right-hand side
-// and two solution copies [3][6bw], pivot inverses + one L column [2][bw][36], two backward rings
-// xr/part [4][bw+1][6]; then the x_p staging [nf][6].
+// the LDS from 0: the separator's L blocks [bw(bw-1)/2][36], pivot inverses [bw][36], the
+// current pivot column [2][bw][36] and pivot block [2][36] (step parity), its right-hand side and
+// two solution copies [3][6bw]; behind the x_p staging [nf][6] at offset 0 (twisted_lds_bytes:
+// the back substitution's streamed chunks reuse the region, band_backward_stream).
 __host__ __device__ constexpr size_t twisted_merge_doubles(int bw) {
-    return (size_t)(6 * bw) * (6 * bw + 1) / 2 + 3 * (size_t)(6 * bw) + 72 * (size_t)bw + 24 * (size_t)(bw + 1);
+    return (size_t)bw * (bw - 1) / 2 * 36 + 108 * (size_t)bw + 72 + 3 * (size_t)(6 * bw);
 }
 
 template <int BW>
@@ -1912,10 +1982,8 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     // S_0^{-1}, y_0, z_0
     if (crit) {
         bool fail = false;
-        double M = 0.0;
-        if (lane < 36) M = piv[lane];
-        else if (lane < 42) { M = bwin[lane - 36]; ys[lane - 36] = M; }
-        const double I = gj_inverse6(M, lane, fail);
+        if (lane >= 36 && lane < 42) ys[lane - 36] = bwin[lane - 36];
+        const double I = ldl_inverse6(piv, bwin, lane, fail);
         if (lane < 36) { Kv[lane] = I; ringK[lane] = I; }
         else if (lane < 42) ringZ[lane - 36] = I;
         if (fail && lane == 0) s_fail = 1;
@@ -2016,7 +2084,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                     if (!mat) ys[k1b * 6 + r] = M;
                 }
                 bool fail = false;
-                const double I = gj_inverse6(M, lnl, fail);
+                const double I = ldl_inverse6(piv + k1b * 36, ys + k1b * 6, lnl, fail);
                 if (lnl < 36) { Kv[k1b * 36 + lnl] = I; ringK[kRK * 36 + lnl] = I; }
                 else if (lnl < 42) ringZ[kRK * 6 + lnl - 36] = I;
                 // the look-ahead inverse past the last eliminated row (a separator row) is not a pivot
@@ -2257,6 +2325,142 @@ __device__ __forceinline__ void band_backward(const double *Lband, const double 
     }
 }
 
+// Streamed back substitution of the two-sided band kernel for bw >= 11 (6·bw > 64 lanes), both
+// segments at once: wave 0 runs segment 0, wave 1 segment 1, and the other waves stream the rows
+// of L they are about to need into LDS, CH rows a chunk, double-buffered with one workgroup
+// barrier per chunk (the one-wave band_backward waited on its L2 prefetches, two steps ahead at
+// ≈ 2.2 k cycles a step). Right-looking: the wave keeps the z values of the BW rows below the
+// current row i in registers (lane entry t = q·64 + lane: ring slot t/6 = row mod BW, component
+// t%6); once row i is final, x_i is broadcast by v_readlane and every lane removes
+// L_{i,j}ᵀ x_i from its row j = i − w in one 6-term product, reading row i of L (contiguous in
+// Lband: blocks (i, i−1) .. (i, i−BW)) from the staged chunk; row i's slot then takes row i−BW
+// (z_{i−BW} staged with the row). Rows nsteps.. of a segment are the separator (x given).
+struct BackSeg {
+    const double *Lband, *zb, *xsep;  // segment's L rows and z, its separator x [BW][6]
+    int nsteps;                       // eliminated rows (x written for rows < nsteps)
+    bool reversed;                    // row i is pose nf-1-i
+};
+__host__ __device__ constexpr int bstream_ch(int bw) { return bw <= 24 ? 4 : 3; }
+__host__ __device__ constexpr size_t bstream_doubles(int bw) {
+    return (size_t)4 * bstream_ch(bw) * ((size_t)bw * 36 + 6);  // [2 buffers][2 segments][CH][RS]
+}
+template <int BW, int NT>
+__device__ __forceinline__ void band_backward_stream(const BackSeg (&sg)[2], int nrows, int nf, double *xl, double *buf) {
+    constexpr int RS = BW * 36 + 6, CH = bstream_ch(BW), NQ = (BW * 6 + 63) / 64;
+    constexpr int SEG = CH * RS;                       // doubles of one segment's chunk
+    constexpr int PN = NT - 128, NP2 = SEG;            // producer threads; double2 pieces of a chunk
+    constexpr int PER = (NP2 + PN - 1) / PN;           // pieces per producer thread
+    static_assert(RS % 2 == 0 && PN > 0, "staged rows are double2 pieces");
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int last0 = min(nrows - 1, sg[0].nsteps - 1 + BW), last1 = min(nrows - 1, sg[1].nsteps - 1 + BW);
+    const double *L0 = sg[0].Lband, *L1 = sg[1].Lband, *z0 = sg[0].zb, *z1 = sg[1].zb;
+    const int nchunk = (max(last0, last1) + CH) / CH;  // chunk c: rows last - c·CH .. last - c·CH - CH + 1
+    // producers: both segments' rows of chunk c, loaded into registers one chunk period before
+    // they are stored (the loads stay in flight across the LDS-only barrier)
+    const int pt = tid - 128;
+    double2 v[PER];
+    auto load_chunk = [&](int c) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int e = pt + j * PN;                 // piece: segment e / (SEG/2), offset 2·(e % (SEG/2))
+            v[j] = make_double2(0.0, 0.0);
+            if (e < NP2) {
+                const int s = e / (SEG / 2), o2 = 2 * (e % (SEG / 2)), u = o2 / RS, o = o2 % RS;
+                const int i = (s ? last1 : last0) - (c * CH + u);
+                if (i >= 0) {
+                    const double *Lb = s ? L1 : L0, *zb = s ? z1 : z0;  // (no runtime index into sg: stack)
+                    if (o < BW * 36) v[j] = *(const double2 *)(Lb + ((size_t)i * (BW + 1) + 1) * 36 + o);
+                    else if (i - BW >= 0) v[j] = *(const double2 *)(zb + (size_t)(i - BW) * 6 + (o - BW * 36));
+                }
+            }
+        }
+    };
+    auto store_chunk = [&](int c) {
+        double2 *dst = (double2 *)(buf + (size_t)(c & 1) * 2 * SEG);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int e = pt + j * PN;
+            if (e < NP2) dst[e] = v[j];
+        }
+    };
+    // ---- consumer state: the ring of the segment's z (rows last-BW+1 .. last at the start)
+    const bool cons = wv < 2, s1 = wv == 1;
+    const double *gz = s1 ? z1 : z0, *gx = s1 ? sg[1].xsep : sg[0].xsep;
+    const bool grev = s1 ? sg[1].reversed : sg[0].reversed;
+    const int last = s1 ? last1 : last0, ns = s1 ? sg[1].nsteps : sg[0].nsteps;
+    const int lastu = __builtin_amdgcn_readfirstlane(last);  // (per wave)
+    double z[NQ];
+    int ws[NQ];                                        // w = i - j of the entry's row j at step i
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int t = q * 64 + lane, sl = t / 6, r = t % 6;
+        z[q] = 0.0;
+        ws[q] = 0;
+        if (cons && t < BW * 6) {
+            const int j = last - (((last - sl) % BW) + BW) % BW;
+            ws[q] = last - j;
+            if (j >= ns) z[q] = gx[(j - ns) * 6 + r];
+            else if (j >= 0) z[q] = gz[(size_t)j * 6 + r];
+        }
+    }
+    if (wv >= 2) load_chunk(0);
+    __syncthreads();  // (the separator x sits in the region the chunks overwrite)
+    if (wv >= 2) {
+        store_chunk(0);
+        if (1 < nchunk) load_chunk(1);
+    }
+    lds_barrier();
+    for (int c = 0; c < nchunk; ++c) {
+        if (wv >= 2) {
+            if (c + 1 < nchunk) store_chunk(c + 1);
+            if (c + 2 < nchunk) load_chunk(c + 2);
+        } else if (cons) {
+            const double *B = buf + ((size_t)(c & 1) * 2 + wv) * SEG;
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = lastu - (c * CH + u);  // (uniform: scalar slot arithmetic below)
+                if (i < 0) break;
+                const double *Lr = B + u * RS;
+                // the step's L reads first: they do not depend on x_i (a slot whose row is final
+                // this step reads block BW, row i-BW's, and the staged z_{i-BW})
+                double Lv[NQ][6], zr[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int r = (q * 64 + lane) % 6, w = ws[q] == 0 ? BW : ws[q];
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) Lv[q][m] = Lr[(w - 1) * 36 + m * 6 + r];
+                    zr[q] = Lr[BW * 36 + r];
+                }
+                const int si = i % BW;
+                double x[6];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {  // x_i from the lanes of row i's slot
+                    const int t = si * 6 + r, q = t >> 6, ln = t & 63;
+                    double v = z[0];
+#pragma unroll
+                    for (int qq = 1; qq < NQ; ++qq) v = q == qq ? z[qq] : v;
+                    x[r] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), ln),
+                                            __builtin_amdgcn_readlane(__double2loint(v), ln));
+                }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int t = q * 64 + lane, r = t % 6;
+                    const bool fin = ws[q] == 0;   // row i: final; the slot takes row i - BW
+                    const int w = fin ? BW : ws[q], j = i - w;
+                    if (fin && t < BW * 6 && i < ns) xl[(size_t)(grev ? nf - 1 - i : i) * 6 + r] = z[q];
+                    double acc = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) acc = fma(Lv[q][m], x[m], acc);
+                    const double zz = fin ? zr[q] : z[q];
+                    z[q] = (j >= 0 && j < ns) ? zz - acc : zz;
+                    ws[q] = w - 1;
+                }
+            }
+        }
+        lds_barrier();
+    }
+}
+
 template <int BW>
 __global__ __launch_bounds__(band_nt(BW)) void k_rcs_factor_band(Dev d0) {
     TRIAL_SLOT(blockIdx.y)
@@ -2329,81 +2533,117 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
     if (!s_sfail) {
     // merge layout (twisted_merge_doubles) from LDS offset 0: the band windows are dead, both
     // separators having been exported to global memory before the arrival
-    constexpr int NP = NS * (NS + 1) / 2;
-    double *Mp = lds;                                  // [NP] packed lower triangle, scalar rows
-    double *rhs = Mp + NP, *xs0 = rhs + NS, *xsr = xs0 + NS;  // [NS] each
-    double *Kp = xsr + NS, *Fb = Kp + (size_t)BW * 36;  // [BW][36] pivot inverses, [BW][36] L column
-    double *xr = Fb + (size_t)BW * 36, *part = xr + W * 6, *xr1 = part + W * 6, *part1 = xr1 + W * 6;
-    double *xl = lds + twisted_merge_doubles(BW);  // [nf][6] x_p staging
-    auto mp = [&](int r, int c) -> double & { return Mp[r * (r + 1) / 2 + c]; };  // r >= c
-    // ---- separator system S_sep (lower block (i,j), i >= j, w = i-j) and its right-hand side
+    double *xl = lds;                                  // [nf][6] x_p staging
+    double *Ls = lds + (size_t)d.nf * 6;               // [BW(BW-1)/2][36] L_IP, I > P (block I(I-1)/2 + P)
+    double *Kp = Ls + (size_t)BW * (BW - 1) / 2 * 36;  // [BW][36] pivot inverses S_PP⁻¹
+    double *colA = Kp + (size_t)BW * 36;               // [2][BW][36] pivot column A_IP (step parity)
+    double *pv = colA + (size_t)2 * BW * 36;           // [2][36] pivot block S_PP (step parity)
+    double *rhs = pv + 72, *xs0 = rhs + NS, *xsr = xs0 + NS;  // [NS] each
+    // Separator system S_sep (lower block (I, J), I >= J, w = I - J < BW) by right-looking block
+    // LDLᵀ with the blocks held in registers: block (I, J) is owned by UPB threads (UR rows each,
+    // the band kernel's split) for the whole elimination, so a trailing update reads only its
+    // L_IP rows and A_JP from LDS (54 reads for 108 FMA at UR = 3) and writes nothing back. Per
+    // pivot P three barriers: wave 0 inverts S_PP; the owners of column P form L_IP = A_IP S_PP⁻¹;
+    // the owners of the trailing blocks apply A_IJ -= L_IP A_JPᵀ and publish column P + 1 into
+    // the other parity buffer (the right-hand side y_R -= L_RP y_P on the side). No pivoting: a zero LDLᵀ pivot fails the
+    // solve as SimplicialLDLT does. (Round 5 held the system as a packed scalar triangle in LDS and
+    // swept it with one thread per entry: runtime divisions + 12 LDS reads per FMA-6 entry;
+    // ≈ 28 % of the C3R factorisation.)
     const double *W0 = d.tw_sep, *W1 = d.tw_sep + sep_stride;
-    for (int t = tid; t < NS * NS; t += NT) {
-        const int hi = t / NS, lo = t % NS;
-        if (lo > hi) continue;
-        const int i = hi / 6, a = hi % 6, j = lo / 6, b = lo % 6, w = i - j;
-        double v;
-        if (w > BW) v = 0.0;
-        else {
-            const double w0 = W0[((size_t)i * W + w) * 36 + a * 6 + b];
-            const double w1 = W1[((size_t)(BW - 1 - j) * W + w) * 36 + b * 6 + a];
-            const double a0 = d.Bd[((size_t)(m + i) * W + w) * 36 + a * 6 + b];
-            v = w0 + w1 - a0;
-        }
-        mp(hi, lo) = v;
+    constexpr int UR = band_ur(BW), UPB = 6 / UR, UE = UR * 6, NB = BW * (BW + 1) / 2;
+    static_assert(UPB * NB <= NT, "one owned separator (part) block per thread");
+    const bool own = tid < UPB * NB;
+    int oI = 0, oJ = 0;
+    if (own) {
+        const int b = tid / UPB;
+        while ((oI + 1) * (oI + 2) / 2 <= b) ++oI;
+        oJ = b - oI * (oI + 1) / 2;
     }
-    for (int t = tid; t < NS; t += NT) {
-        const int i = t / 6, a = t % 6;
-        rhs[t] = W0[(size_t)BW * W * 36 + i * 6 + a] + W1[(size_t)BW * W * 36 + (BW - 1 - i) * 6 + a] -
+    const int oh = (tid % UPB) * UR;  // first row of the owned part
+    double t[UE];
+    if (own) {
+        const int w = oI - oJ;
+#pragma unroll
+        for (int r = 0; r < UR; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                const int a = oh + r;
+                const double w0 = W0[((size_t)oI * W + w) * 36 + a * 6 + c];
+                t[r * 6 + c] = w0 + W1[((size_t)(BW - 1 - oJ) * W + w) * 36 + c * 6 + a] -
+                               d.Bd[((size_t)(m + oI) * W + w) * 36 + a * 6 + c];
+            }
+        // column 0: the first pivot block / pivot column
+        if (oJ == 0) {
+            double *dst = oI == 0 ? pv : colA + (size_t)oI * 36;
+#pragma unroll
+            for (int j = 0; j < UE; ++j) dst[oh * 6 + j] = t[j];
+        }
+    }
+    for (int q = tid; q < NS; q += NT) {
+        const int i = q / 6, a = q % 6;
+        rhs[q] = W0[(size_t)BW * W * 36 + i * 6 + a] + W1[(size_t)BW * W * 36 + (BW - 1 - i) * 6 + a] -
                  d.bs[(size_t)(m + i) * 6 + a];
     }
     if (tid == 0) s_sfail = 0;
     __syncthreads();
-    // block LDLᵀ with 6x6 pivots on the packed lower triangle (no pivoting: the pivots are LDLᵀ
-    // pivots, a zero one fails the solve as SimplicialLDLT does); wave 0 inverts the pivot block,
-    // L_IP = A_IP S_PP⁻¹ goes to Fb, every trailing block and the right-hand side are updated in
-    // one parallel pass, then L_IP replaces A_IP in the triangle for the back substitution
     for (int P = 0; P < BW; ++P) {
-        if (tid < 64) {
+        const double *pvP = pv + (P & 1) * 36, *colP = colA + (size_t)(P & 1) * BW * 36;
+        if (tid < 64) {  // S_PP⁻¹ (lane-local LDLᵀ, every lane the same pivots)
             bool f = false;
-            const int a = tid / 6, b = tid % 6;
-            const double M = tid < 36 ? (a >= b ? mp(P * 6 + a, P * 6 + b) : mp(P * 6 + b, P * 6 + a)) : 0.0;
-            const double I = gj_inverse6(M, tid, f);
+            const double I = ldl_inverse6(pvP, rhs, tid, f);
             if (tid < 36) Kp[P * 36 + tid] = I;
             if (f && tid == 0) s_sfail = 1;
         }
         __syncthreads();
         if (s_sfail) break;
-        for (int t = tid; t < (BW - 1 - P) * 36; t += NT) {  // L_IP = A_IP · S_PP⁻¹, I > P
-            const int I = P + 1 + t / 36, e = t % 36, a_ = e / 6, b_ = e % 6;
-            double acc = 0.0;
+        if (own && oJ == P && oI > P) {  // L_IP = A_IP S_PP⁻¹ (rows oh..oh+UR-1)
+            const double *K = Kp + P * 36;
+            double *L = Ls + ((size_t)oI * (oI - 1) / 2 + P) * 36 + oh * 6;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) acc = fma(mp(I * 6 + a_, P * 6 + q), Kp[P * 36 + q * 6 + b_], acc);
-            Fb[(I - P - 1) * 36 + e] = acc;
+            for (int r = 0; r < UR; ++r)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) acc = fma(t[r * 6 + q], K[q * 6 + c], acc);
+                    L[r * 6 + c] = acc;
+                }
         }
         __syncthreads();
-        const int nr = NS - (P + 1) * 6;  // trailing rows / columns
-        for (int t = tid; t < nr * (nr + 1); t += NT) {
-            const int rr = t / (nr + 1), cc = t % (nr + 1);
-            const int R_ = (P + 1) * 6 + rr;
-            if (cc == nr) {  // right-hand side: y_R -= L_R,P · y_P
+        if (own && oJ > P) {  // A_IJ -= L_IP A_JPᵀ, then column P + 1 published
+            const double *L = Ls + ((size_t)oI * (oI - 1) / 2 + P) * 36 + oh * 6;
+            const double *Aj = colP + (size_t)oJ * 36;
+            double l[UE];
+#pragma unroll
+            for (int j = 0; j < UE; ++j) l[j] = L[j];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                double a[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) a[q] = Aj[c * 6 + q];
+#pragma unroll
+                for (int r = 0; r < UR; ++r) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) acc = fma(l[r * 6 + q], a[q], acc);
+                    t[r * 6 + c] -= acc;
+                }
+            }
+        }
+        {   // y_R -= L_RP y_P for the trailing rows (threads past the owners first)
+            const int q = NT - 1 - tid, R = (P + 1) * 6 + q;
+            if (q >= 0 && R < NS) {
+                const double *L = Ls + ((size_t)(R / 6) * (R / 6 - 1) / 2 + P) * 36 + (R % 6) * 6;
                 double acc = 0.0;
 #pragma unroll
-                for (int q = 0; q < 6; ++q) acc = fma(Fb[(R_ / 6 - P - 1) * 36 + (R_ % 6) * 6 + q], rhs[P * 6 + q], acc);
-                rhs[R_] -= acc;
-                continue;
+                for (int c = 0; c < 6; ++c) acc = fma(L[c], rhs[P * 6 + c], acc);
+                rhs[R] -= acc;
             }
-            const int C_ = (P + 1) * 6 + cc;
-            if (C_ > R_) continue;
-            double acc = 0.0;  // A_RC -= L_R,P · A_C,Pᵀ
-#pragma unroll
-            for (int q = 0; q < 6; ++q) acc = fma(Fb[(R_ / 6 - P - 1) * 36 + (R_ % 6) * 6 + q], mp(C_, P * 6 + q), acc);
-            mp(R_, C_) -= acc;
         }
-        __syncthreads();
-        for (int t = tid; t < (BW - 1 - P) * 36; t += NT) {
-            const int I = P + 1 + t / 36, e = t % 36;
-            mp(I * 6 + e / 6, P * 6 + e % 6) = Fb[(I - P - 1) * 36 + e];
+        if (own && oJ == P + 1) {
+            double *dst = oI == P + 1 ? pv + ((P + 1) & 1) * 36 : colA + ((size_t)((P + 1) & 1) * BW + oI) * 36;
+#pragma unroll
+            for (int j = 0; j < UE; ++j) dst[oh * 6 + j] = t[j];
         }
         __syncthreads();
     }
@@ -2412,27 +2652,40 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
     TW_MARK(2, tw_t2 - tw_t1);
 #endif
     if (!s_sfail) {
-    // back substitution x_P = S_PP⁻¹ y_P − Σ_{I>P} L_IPᵀ x_I; x_sep in both segment orders: rows m+i
-    // for segment 0, reversed rows n1+i = original m+BW-1-i for segment 1
-    for (int P = BW - 1; P >= 0; --P) {
-        if (tid < 6) {
-            double x = 0.0;
+    // back substitution x_P = S_PP⁻¹ y_P − Σ_{I>P} L_IPᵀ x_I, right-looking: x_I is final once the
+    // blocks below it are done, and its contribution is removed from every P < I in one pass.
+    // x_sep in both segment orders: rows m+i for segment 0, reversed rows n1+i = original
+    // m+BW-1-i for segment 1
+    for (int q = tid; q < NS; q += NT) {
+        const int P = q / 6, c = q % 6;
+        double x = 0.0;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) x = fma(Kp[P * 36 + tid * 6 + q], rhs[P * 6 + q], x);
-            for (int R_ = (P + 1) * 6; R_ < NS; ++R_) x -= mp(R_, P * 6 + tid) * xs0[R_];
-            xs0[P * 6 + tid] = x;
-            xl[(size_t)m * 6 + P * 6 + tid] = x;
+        for (int r = 0; r < 6; ++r) x = fma(Kp[P * 36 + c * 6 + r], rhs[P * 6 + r], x);
+        xs0[q] = x;
+    }
+    __syncthreads();
+    for (int I = BW - 1; I >= 1; --I) {
+        if (tid < I * 6) {
+            const int P = tid / 6, c = tid % 6;
+            const double *L = Ls + ((size_t)I * (I - 1) / 2 + P) * 36 + c;
+            double acc = 0.0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) acc = fma(L[r * 6], xs0[I * 6 + r], acc);
+            xs0[tid] -= acc;
         }
         __syncthreads();
     }
-    for (int t = tid; t < NS; t += NT) xsr[t] = xs0[(BW - 1 - t / 6) * 6 + t % 6];
+    for (int q = tid; q < NS; q += NT) {
+        xl[(size_t)m * 6 + q] = xs0[q];
+        xsr[q] = xs0[(BW - 1 - q / 6) * 6 + q % 6];
+    }
     __syncthreads();
     if constexpr (BW * 6 <= 64) {
         if (tid < 64) band_backward_rl<BW, true>(d.Lband, d.zb, m, d.nf, xs0, xl, false, d.nf, tid);
         else if (tid < 128) band_backward_rl<BW, true>(d.Lband2, d.zb2, n1, d.nf, xsr, xl, true, d.nf, tid - 64);
     } else {
-        if (tid < 64) band_backward<BW>(d.Lband, d.zb, m, d.nf, xs0, xl, false, d.nf, xr, part, tid);
-        else if (tid < 128) band_backward<BW>(d.Lband2, d.zb2, n1, d.nf, xsr, xl, true, d.nf, xr1, part1, tid - 64);
+        const BackSeg sg[2] = {{d.Lband, d.zb, xs0, m, false}, {d.Lband2, d.zb2, xsr, n1, true}};
+        band_backward_stream<BW, NT>(sg, d.nf, d.nf, xl, Ls);
     }
     __syncthreads();
     for (int t = tid; t < d.nf * 6; t += NT) d.xp[t] = xl[t];
