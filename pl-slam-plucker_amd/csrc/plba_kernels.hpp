@@ -2325,7 +2325,7 @@ __device__ __forceinline__ void band_backward(const double *Lband, const double 
     }
 }
 
-// Streamed back substitution of the two-sided band kernel for bw >= 11 (6·bw > 64 lanes), both
+// Streamed back substitution of the two-sided register-window band kernel (bw >= 11), both
 // segments at once: wave 0 runs segment 0, wave 1 segment 1, and the other waves stream the rows
 // of L they are about to need into LDS, CH rows a chunk, double-buffered with one workgroup
 // barrier per chunk (the one-wave band_backward waited on its L2 prefetches, two steps ahead at
@@ -2338,21 +2338,22 @@ __device__ __forceinline__ void band_backward(const double *Lband, const double 
 struct BackSeg {
     const double *Lband, *zb, *xsep;  // segment's L rows and z, its separator x [BW][6]
     int nsteps;                       // eliminated rows (x written for rows < nsteps)
+    int nrows;                        // rows of the segment's band (separator included)
     bool reversed;                    // row i is pose nf-1-i
 };
 __host__ __device__ constexpr int bstream_ch(int bw) { return bw <= 24 ? 4 : 3; }
 __host__ __device__ constexpr size_t bstream_doubles(int bw) {
     return (size_t)4 * bstream_ch(bw) * ((size_t)bw * 36 + 6);  // [2 buffers][2 segments][CH][RS]
 }
-template <int BW, int NT>
-__device__ __forceinline__ void band_backward_stream(const BackSeg (&sg)[2], int nrows, int nf, double *xl, double *buf) {
-    constexpr int RS = BW * 36 + 6, CH = bstream_ch(BW), NQ = (BW * 6 + 63) / 64;
+template <int BW, int NT, int CH>
+__device__ __forceinline__ void band_backward_stream(const BackSeg (&sg)[2], int nf, double *xl, double *buf) {
+    constexpr int RS = BW * 36 + 6, NQ = (BW * 6 + 63) / 64;  // buf: [2][2][CH][RS]
     constexpr int SEG = CH * RS;                       // doubles of one segment's chunk
     constexpr int PN = NT - 128, NP2 = SEG;            // producer threads; double2 pieces of a chunk
     constexpr int PER = (NP2 + PN - 1) / PN;           // pieces per producer thread
     static_assert(RS % 2 == 0 && PN > 0, "staged rows are double2 pieces");
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int last0 = min(nrows - 1, sg[0].nsteps - 1 + BW), last1 = min(nrows - 1, sg[1].nsteps - 1 + BW);
+    const int last0 = min(sg[0].nrows - 1, sg[0].nsteps - 1 + BW), last1 = min(sg[1].nrows - 1, sg[1].nsteps - 1 + BW);
     const double *L0 = sg[0].Lband, *L1 = sg[1].Lband, *z0 = sg[0].zb, *z1 = sg[1].zb;
     const int nchunk = (max(last0, last1) + CH) / CH;  // chunk c: rows last - c·CH .. last - c·CH - CH + 1
     // producers: both segments' rows of chunk c, loaded into registers one chunk period before
@@ -2684,8 +2685,8 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
         if (tid < 64) band_backward_rl<BW, true>(d.Lband, d.zb, m, d.nf, xs0, xl, false, d.nf, tid);
         else if (tid < 128) band_backward_rl<BW, true>(d.Lband2, d.zb2, n1, d.nf, xsr, xl, true, d.nf, tid - 64);
     } else {
-        const BackSeg sg[2] = {{d.Lband, d.zb, xs0, m, false}, {d.Lband2, d.zb2, xsr, n1, true}};
-        band_backward_stream<BW, NT>(sg, d.nf, d.nf, xl, Ls);
+        const BackSeg sg[2] = {{d.Lband, d.zb, xs0, m, d.nf, false}, {d.Lband2, d.zb2, xsr, n1, d.nf, true}};
+        band_backward_stream<BW, NT, bstream_ch(BW)>(sg, d.nf, xl, Ls);
     }
     __syncthreads();
     for (int t = tid; t < d.nf * 6; t += NT) d.xp[t] = xl[t];
