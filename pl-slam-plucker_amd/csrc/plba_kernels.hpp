@@ -1890,14 +1890,16 @@ __host__ __device__ constexpr size_t band_lds_doubles(int bw, int R) {
 // side) plus a few flags. A separate LDS object from the dynamic window, so that the compiler can
 // tell the direct global->LDS loads into it from the window's reads (with one LDS object every
 // ds_read after such a load waits for it)
-__host__ __device__ constexpr size_t band_static_bytes(int bw) { return 16 * ((size_t)(bw + 1) * 36 + 6) + 64; }
+__host__ __device__ constexpr size_t band_static_bytes(int bw) {
+    return 16 * ((size_t)(bw + 1) * 36 + 6) + 64;
+}
 // The twisted kernel's merge, after both segments have exported their separator windows, reuses
 // the LDS from 0: the separator's L blocks [bw(bw-1)/2][36], pivot inverses [bw][36], the
-// current pivot column [2][bw][36] and pivot block [2][36] (step parity), its right-hand side and
+// current pivot column [2][bw][36] (step parity), the pivot blocks [bw][36], its right-hand side and
 // two solution copies [3][6bw]; behind the x_p staging [nf][6] at offset 0 (twisted_lds_bytes:
 // the back substitution's streamed chunks reuse the region, band_backward_stream).
 __host__ __device__ constexpr size_t twisted_merge_doubles(int bw) {
-    return (size_t)bw * (bw - 1) / 2 * 36 + 108 * (size_t)bw + 72 + 3 * (size_t)(6 * bw);
+    return (size_t)bw * (bw - 1) / 2 * 36 + 144 * (size_t)bw + 3 * (size_t)(6 * bw);
 }
 
 template <int BW>
@@ -1995,6 +1997,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
     int sk = 0, kR = 0, kRK = 1;                  // k % W (rhs row slots), k % R, (k+1) % RK
+    int fr0 = 0;                                  // (first step of the current flush batch) % RK
     // a zero pivot sets s_fail and the sweep runs on (inf/NaN blocks are never used: the
     // caller drops the solve); no per-step LDS read of the flag on the critical chain
     for (int k = 0; k < nsteps; ++k) {
@@ -2002,8 +2005,11 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         // the step (a few integer ops) instead of being hoisted out of the loop as dozens of
         // loop-invariant registers that then spill to scratch (a scratch reload waits for every
         // outstanding global load, the spare-slot loads included)
-        int wtl = wt, lnl = lane, owl = ow, ohl = oh, oCl = oC;
-        asm volatile("" : "+v"(wtl), "+v"(lnl), "+v"(owl), "+v"(ohl), "+v"(oCl));
+        // (the lane index is re-derived from v_mbcnt each step: carried, it was spilled and its
+        // scratch reload at the step top stalled the critical wave on vmcnt)
+        int wtl = wt, owl = ow, ohl = oh, oCl = oC;
+        asm volatile("" : "+v"(wtl), "+v"(owl), "+v"(ohl), "+v"(oCl));
+        const int lnl = (int)__lane_id();
         const int kb = k & 1;
         const int wmax = min(BW, nrows - 1 - k);
         const double *Kk = Kv + kb * 36;
@@ -2061,7 +2067,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         lds_barrier();
         STAMP(2);
         // ---- phase 2 (the worker waves first put row k+W+1 in flight)
-        if (!crit) stage_row(k + W + 1, (tid >> 6) - 1, lnl);
+        if (!crit) stage_row(k + W + 1, __builtin_amdgcn_readfirstlane(tid >> 6) - 1, lnl);  // (wave index in an SGPR)
         if (crit) {
             if (k + 1 < nrows) {
                 const int s1 = slot(1), k1b = kb ^ 1;
@@ -2149,9 +2155,16 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
                         const int i = k0 + st + w;
                         if (i < nrows) g.Lband[((size_t)i * W + w) * 36 + e] = ringL[(size_t)st * BW * 36 + rem];
                     }
-                for (int t2 = wtl; t2 < cnt * 36; t2 += NW)
-                    g.Kinv[(size_t)k0 * 36 + t2] = ringK[((k0 + t2 / 36) % RK) * 36 + t2 % 36];
-                for (int t2 = wtl; t2 < cnt * 6; t2 += NW) g.zb[(size_t)k0 * 6 + t2] = ringZ[((k0 + t2 / 6) % RK) * 6 + t2 % 6];
+                const int r0 = fr0;      // k0 mod RK, kept incrementally (a per-lane division by the
+                fr0 = fr0 + R >= RK ? fr0 + R - RK : fr0 + R;  // runtime ring size spilled its magic number)
+                for (int t2 = wtl; t2 < cnt * 36; t2 += NW) {
+                    const int sl = r0 + t2 / 36;
+                    g.Kinv[(size_t)k0 * 36 + t2] = ringK[(sl >= RK ? sl - RK : sl) * 36 + t2 % 36];
+                }
+                for (int t2 = wtl; t2 < cnt * 6; t2 += NW) {
+                    const int sl = r0 + t2 / 6;
+                    g.zb[(size_t)k0 * 6 + t2] = ringZ[(sl >= RK ? sl - RK : sl) * 6 + t2 % 6];
+                }
             }
             STAMP(7);
             // the staged row lands before the barrier (issued at the start of this phase; read at
@@ -2536,18 +2549,20 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
     // separators having been exported to global memory before the arrival
     double *xl = lds;                                  // [nf][6] x_p staging
     double *Ls = lds + (size_t)d.nf * 6;               // [BW(BW-1)/2][36] L_IP, I > P (block I(I-1)/2 + P)
-    double *Kp = Ls + (size_t)BW * (BW - 1) / 2 * 36;  // [BW][36] pivot inverses S_PP⁻¹
+    double *Kp = Ls + (size_t)BW * (BW - 1) / 2 * 36;  // [BW][36] pivot inverses S_PP⁻¹ (after the sweep)
     double *colA = Kp + (size_t)BW * 36;               // [2][BW][36] pivot column A_IP (step parity)
-    double *pv = colA + (size_t)2 * BW * 36;           // [2][36] pivot block S_PP (step parity)
-    double *rhs = pv + 72, *xs0 = rhs + NS, *xsr = xs0 + NS;  // [NS] each
+    double *Sp = colA + (size_t)2 * BW * 36;           // [BW][36] pivot blocks S_PP
+    double *rhs = Sp + (size_t)BW * 36, *xs0 = rhs + NS, *xsr = xs0 + NS;  // [NS] each
     // Separator system S_sep (lower block (I, J), I >= J, w = I - J < BW) by right-looking block
     // LDLᵀ with the blocks held in registers: block (I, J) is owned by UPB threads (UR rows each,
     // the band kernel's split) for the whole elimination, so a trailing update reads only its
     // L_IP rows and A_JP from LDS (54 reads for 108 FMA at UR = 3) and writes nothing back. Per
-    // pivot P three barriers: wave 0 inverts S_PP; the owners of column P form L_IP = A_IP S_PP⁻¹;
-    // the owners of the trailing blocks apply A_IJ -= L_IP A_JPᵀ and publish column P + 1 into
-    // the other parity buffer (the right-hand side y_R -= L_RP y_P on the side). No pivoting: a zero LDLᵀ pivot fails the
-    // solve as SimplicialLDLT does. (Round 5 held the system as a packed scalar triangle in LDS and
+    // pivot P two barriers: the owners of column P factor S_PP LDLᵀ in their own registers and
+    // solve their rows of L_IP = A_IP S_PP⁻¹; the owners of the trailing blocks apply
+    // A_IJ -= L_IP A_JPᵀ and publish column P + 1 into the other parity buffer (the right-hand
+    // side y_R -= L_RP y_P on the side). The pivot inverses the back substitution needs are formed
+    // after the sweep, all at once (a wave-0 inverse per step was one more barrier and ≈ 1 k cycles
+    // on the chain). No pivoting: a zero LDLᵀ pivot fails the solve as SimplicialLDLT does. (Round 5 held the system as a packed scalar triangle in LDS and
     // swept it with one thread per entry: runtime divisions + 12 LDS reads per FMA-6 entry;
     // ≈ 28 % of the C3R factorisation.)
     const double *W0 = d.tw_sep, *W1 = d.tw_sep + sep_stride;
@@ -2575,7 +2590,7 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
             }
         // column 0: the first pivot block / pivot column
         if (oJ == 0) {
-            double *dst = oI == 0 ? pv : colA + (size_t)oI * 36;
+            double *dst = oI == 0 ? Sp : colA + (size_t)oI * 36;
 #pragma unroll
             for (int j = 0; j < UE; ++j) dst[oh * 6 + j] = t[j];
         }
@@ -2587,28 +2602,30 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
     }
     if (tid == 0) s_sfail = 0;
     __syncthreads();
+#ifdef PLBA_STAMPS
+    TW_MARK(5, __builtin_readcyclecounter() - tw_t1);  // hand-off + separator assembly
+#endif
     for (int P = 0; P < BW; ++P) {
-        const double *pvP = pv + (P & 1) * 36, *colP = colA + (size_t)(P & 1) * BW * 36;
-        if (tid < 64) {  // S_PP⁻¹ (lane-local LDLᵀ, every lane the same pivots)
-            bool f = false;
-            const double I = ldl_inverse6(pvP, rhs, tid, f);
-            if (tid < 36) Kp[P * 36 + tid] = I;
-            if (f && tid == 0) s_sfail = 1;
-        }
-        __syncthreads();
-        if (s_sfail) break;
-        if (own && oJ == P && oI > P) {  // L_IP = A_IP S_PP⁻¹ (rows oh..oh+UR-1)
-            const double *K = Kp + P * 36;
+        const double *colP = colA + (size_t)(P & 1) * BW * 36;
+        if (own && oJ == P && oI > P) {  // rows oh..oh+UR-1 of L_IP = A_IP S_PP⁻¹ (S symmetric: S⁻¹ a_r)
+            const double *S = Sp + P * 36;
+            double s[21], dv[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = 0; j <= i; ++j) s[ltri(i, j)] = S[i * 6 + j];
+            bool zp = false;  // (a zero pivot is reported by the inverses below)
+            ldl6_inplace(s, dv, zp);
             double *L = Ls + ((size_t)oI * (oI - 1) / 2 + P) * 36 + oh * 6;
 #pragma unroll
-            for (int r = 0; r < UR; ++r)
+            for (int r = 0; r < UR; ++r) {
+                double x[6];
 #pragma unroll
-                for (int c = 0; c < 6; ++c) {
-                    double acc = 0.0;
+                for (int c = 0; c < 6; ++c) x[c] = t[r * 6 + c];
+                ldl6_solve(s, dv, x);
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) acc = fma(t[r * 6 + q], K[q * 6 + c], acc);
-                    L[r * 6 + c] = acc;
-                }
+                for (int c = 0; c < 6; ++c) L[r * 6 + c] = x[c];
+            }
         }
         __syncthreads();
         if (own && oJ > P) {  // A_IJ -= L_IP A_JPᵀ, then column P + 1 published
@@ -2642,12 +2659,19 @@ __device__ __forceinline__ void k_rcs_factor_twisted_body(const Dev &d) {
             }
         }
         if (own && oJ == P + 1) {
-            double *dst = oI == P + 1 ? pv + ((P + 1) & 1) * 36 : colA + ((size_t)((P + 1) & 1) * BW + oI) * 36;
+            double *dst = oI == P + 1 ? Sp + (P + 1) * 36 : colA + ((size_t)((P + 1) & 1) * BW + oI) * 36;
 #pragma unroll
             for (int j = 0; j < UE; ++j) dst[oh * 6 + j] = t[j];
         }
         __syncthreads();
     }
+    for (int P = tid >> 6; P < BW; P += NT / 64) {  // S_PP⁻¹, one pivot block per wave
+        bool f = false;
+        const double I = ldl_inverse6(Sp + P * 36, rhs, tid & 63, f);
+        if ((tid & 63) < 36) Kp[P * 36 + (tid & 63)] = I;
+        if (f && (tid & 63) == 0) s_sfail = 1;
+    }
+    __syncthreads();
 #ifdef PLBA_STAMPS
     unsigned long long tw_t2 = __builtin_readcyclecounter();
     TW_MARK(2, tw_t2 - tw_t1);

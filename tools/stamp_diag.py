@@ -44,4 +44,4 @@ if st.get("column_lane") and st["twisted"]:
 elif tw[4] > 0:
     n = tw[4]
     print(f"twisted (per launch, s_memtime/readcyclecounter units): fwd seg0 {tw[0]/n:.0f} fwd seg1 {tw[1]/n:.0f} "
-          f"handoff+separator {tw[2]/n:.0f} backward {tw[3]/n:.0f}")
+          f"handoff+separator {tw[2]/n:.0f} (of which hand-off + assembly {tw[5]/n:.0f}) backward {tw[3]/n:.0f}")
