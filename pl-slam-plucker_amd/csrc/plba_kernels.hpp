@@ -1890,9 +1890,11 @@ __host__ __device__ constexpr size_t band_lds_doubles(int bw, int R) {
 // side) plus a few flags. A separate LDS object from the dynamic window, so that the compiler can
 // tell the direct global->LDS loads into it from the window's reads (with one LDS object every
 // ds_read after such a load waits for it)
-__host__ __device__ constexpr size_t band_static_bytes(int bw) {
-    return 16 * ((size_t)(bw + 1) * 36 + 6) + 64;
-}
+// entering-row staging buffers of band_forward: a row is issued at the start of a step's second
+// phase and retired before its last barrier (round 6: a third buffer with the row in flight
+// across the barrier, retired one step later with vmcnt(1), measured 294 -> 303 µs at C3R)
+constexpr int kBandStage = 2;
+__host__ __device__ constexpr size_t band_static_bytes(int bw) { return 8 * kBandStage * ((size_t)(bw + 1) * 36 + 6) + 64; }
 // The twisted kernel's merge, after both segments have exported their separator windows, reuses
 // the LDS from 0: the separator's L blocks [bw(bw-1)/2][36], pivot inverses [bw][36], the
 // current pivot column [2][bw][36] (step parity), the pivot blocks [bw][36], its right-hand side and
@@ -1916,7 +1918,10 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     __shared__ int s_fail;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const bool crit = tid < 64;                   // wave 0
+    // wave index in an SGPR: the loop's wave-0 tests and the staging-row split need no per-lane
+    // register (a VGPR tid carried through the step loop was spilled and reloaded every step)
+    const int wv_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool crit = wv_s == 0;                  // wave 0
     const int wt = tid - 64;                      // worker thread index
     if (tid == 0) s_fail = 0;
     // ---- the (part) block this worker owns: slot p of diagonal w, rows oh/6 .. oh/6+UR-1
@@ -1953,8 +1958,10 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     // registers at the top of step r-BW. No owner register and no spill reload waits on a global
     // load. Past the band's end the last row is loaded again (never read: readers stop at wmax).
     constexpr int RW = W * 36 + 6, NPC = RW / 2;  // doubles per staged row, 16-byte pieces
-    __shared__ __attribute__((aligned(16))) double stgb[2 * RW];
-    auto stage_row = [&](int row, int wv, int lnv) {  // wv: worker wave index (uniform)
+    __shared__ __attribute__((aligned(16))) double stgb[kBandStage * RW];
+    // staging buffer of a row (r mod kBandStage): incremental, no runtime modulo in the loop
+    auto stg = [&](int slot) { return stgb + (size_t)slot * RW; };
+    auto stage_row = [&](int row, int slot, int wv, int lnv) {  // wv: worker wave index (uniform)
       for (int pb = wv * 64; pb < NPC; pb += NW) {  // (more pieces than worker lanes at bw >= 24)
         const int p = pb + lnv;
         if (p < NPC) {
@@ -1964,7 +1971,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
             // before every later ds_read of the window (it cannot tell the LDS objects apart);
             // this load is retired by the explicit vmcnt(0) before the step's last barrier
             const unsigned dst = __builtin_amdgcn_readfirstlane(
-                (unsigned)(size_t)(__attribute__((address_space(3))) double *)(stgb + (size_t)(row & 1) * RW + pb * 2));
+                (unsigned)(size_t)(__attribute__((address_space(3))) double *)(stg(slot) + pb * 2));
             unsigned keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                          : "=&s"(keep)
@@ -1974,7 +1981,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
       }
     };
     if (!crit) {
-        stage_row(W, (tid >> 6) - 1, lane);
+        stage_row(W, W % kBandStage, wv_s - 1, lane);
         // retired here like every later row's (the compiler does not track the inline-asm load,
         // and step 0's phase 2 already copies its diagonal-BW block out of the staging buffer)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1997,6 +2004,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
     int sk = 0, kR = 0, kRK = 1;                  // k % W (rhs row slots), k % R, (k+1) % RK
+    int sB = BW % kBandStage, sW = W % kBandStage; // staging slots of rows k+BW, k+W
     int fr0 = 0;                                  // (first step of the current flush batch) % RK
     // a zero pivot sets s_fail and the sweep runs on (inf/NaN blocks are never used: the
     // caller drops the solve); no per-step LDS read of the flag on the critical chain
@@ -2021,7 +2029,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
             // (bw 1: its block (k+1, k+1) is also this step's next pivot); its right-hand side into
             // its row slot. (Its diagonal-BW block, this step's pivot-column entry, was copied in
             // the previous step: phase 1 reads it before any barrier of this step.)
-            const double *sr = stgb + (size_t)((k + BW) & 1) * RW;
+            const double *sr = stg(sB);  // row k+BW
             if (own && oo == oCl - 2) {
                 const double2 *src = (const double2 *)(sr + owl * 36 + ohl);
                 double2 *D = (BW == 1 && owl == 0) ? (double2 *)(piv + (kb ^ 1) * 36 + ohl) : nullptr;
@@ -2067,7 +2075,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         lds_barrier();
         STAMP(2);
         // ---- phase 2 (the worker waves first put row k+W+1 in flight)
-        if (!crit) stage_row(k + W + 1, __builtin_amdgcn_readfirstlane(tid >> 6) - 1, lnl);  // (wave index in an SGPR)
+        if (!crit) stage_row(k + W + 1, sB, wv_s - 1, lnl);  // (row k+BW's buffer: consumed at the top)
         if (crit) {
             if (k + 1 < nrows) {
                 const int s1 = slot(1), k1b = kb ^ 1;
@@ -2130,7 +2138,7 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
             }
             // the next pivot column's diagonal-BW entry (k+W, k+1), from row k+W's staging buffer
             if (wtl < 18) {
-                const double *cs = stgb + (size_t)((k + W) & 1) * RW + BW * 36;
+                const double *cs = stg(sW) + BW * 36;  // row k+W
                 ((double2 *)(col + ((size_t)(kb ^ 1) * W + BW) * 36))[wtl] = ((const double2 *)cs)[wtl];
             }
             STAMP(5);
@@ -2175,6 +2183,8 @@ __device__ __forceinline__ bool band_forward(const BandSeg &g, double *lds, int 
         lds_barrier();
         STAMP(4);
         sk = (sk + 1 == W) ? 0 : sk + 1;
+        sB = (sB + 1 == kBandStage) ? 0 : sB + 1;
+        sW = (sW + 1 == kBandStage) ? 0 : sW + 1;
         kR = (kR + 1 == R) ? 0 : kR + 1;
         kRK = (kRK + 1 == RK) ? 0 : kRK + 1;
         oo = (oo == 0) ? oCl - 1 : oo - 1;
