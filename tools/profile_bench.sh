@@ -7,9 +7,9 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- \
-    python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_trace.json
+    python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline --no-host-mirror --windows 0 > $OUT/bench_trace.json
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o bench --output-format csv -- \
-    python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_fetch.json
+    python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-host-mirror --windows 0 > $OUT/bench_fetch.json
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o bench --output-format csv -- \
-    python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_write.json
+    python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-host-mirror --windows 0 > $OUT/bench_write.json
 echo done
