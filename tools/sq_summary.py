@@ -23,8 +23,12 @@ def load(path):
 
 def main():
     d = sys.argv[1]
-    sq = load(os.path.join(d, "sq", "bench_counter_collection.csv"))
-    gr = load(os.path.join(d, "grbm", "bench_counter_collection.csv"))
+    flat = os.path.join(d, "pmc_counter_collection.csv")  # (tools/pmc_sq.sh: one pass, no GRBM)
+    if os.path.exists(flat):
+        sq, gr = load(flat), {}
+    else:
+        sq = load(os.path.join(d, "sq", "bench_counter_collection.csv"))
+        gr = load(os.path.join(d, "grbm", "bench_counter_collection.csv"))
     lines = ["kernel                      launches  waves  busy_cyc  wave_cyc  waves/busy  VALU/launch  LDS/launch  VMEM/launch  LDS_conf  GUI_active"]
     def avg(dct, c):
         v = dct.get(c, [])
