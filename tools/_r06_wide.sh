@@ -7,4 +7,3 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -2 gpurun_out/r06/$1_tests.log
 bash tools/ab_env.sh $1_C3R C3R - PLBA_LIB=pl-slam-plucker_amd/libplba_ab.so && \
 bash tools/ab_env.sh $1_C2R C2R - PLBA_LIB=pl-slam-plucker_amd/libplba_ab.so
-timeout -k 10 120 python tools/stamp_diag.py C3R > gpurun_out/r06/$1_stamps.txt 2>&1 && timeout -k 10 120 python tools/stamp_diag.py C2R >> gpurun_out/r06/$1_stamps.txt 2>&1; grep twisted gpurun_out/r06/$1_stamps.txt
