@@ -754,6 +754,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
             mark("device build (RCM order)");
         }
         devb = true;
+        mark("device build (stage 1 proper)");
         if (devb) {
             n_pt = wb.n_pt; n_ln = wb.n_ln; Ep = wb.Ep; El = wb.El;
             ctx->n_free_edges = wb.n_free_edges;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 
@@ -393,6 +395,16 @@ static_assert(sizeof(Stage1) <= sizeof(WindowBuild::s1), "stage-1 layout fits Wi
 int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
     const plba_graph *g = wb.g;
     hipStream_t st = wb.stream;
+    // PLBA_TIMING: phase marks of the stage (each waits for the stream: timing runs only)
+    const bool tmg = getenv("PLBA_TIMING") != nullptr;
+    auto tlast = std::chrono::steady_clock::now();
+    auto tmark = [&](const char *what) {
+        if (!tmg) return;
+        (void)hipStreamSynchronize(st);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[plba stage1] %-24s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - tlast).count());
+        tlast = t;
+    };
     const int nf = wb.nf, n_kf = g->n_kf, np = g->n_pt, nl = g->n_ln, Ep = g->n_ept, El = g->n_eln;
     const int E = Ep + El, L = np + nl;
     size_t total = 0;
@@ -416,6 +428,7 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
     BCHECK(h2d(s.eln_info, g->eln_info, El, st));
     BCHECK(h2d(s.pt_xyz, g->pt_xyz, 3 * (size_t)np, st));
     BCHECK(h2d(s.ln_orth, g->ln_orth, 4 * (size_t)nl, st));
+    tmark("h2d caller arrays");
     BCHECK(hipMemsetAsync(s.first_e, 0x7F, sizeof(int32_t) * std::max(L, 1), st));
     BCHECK(hipMemsetAsync(s.lmin, 0x7F, sizeof(int32_t) * std::max(L, 1), st));
     BCHECK(hipMemsetAsync(s.cnt, 0, sizeof(int32_t) * std::max(L, 1), st));
@@ -435,6 +448,7 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
         hipLaunchKernelGGL(k_b_first_blk, dim3((unsigned)std::min<int64_t>(grid(E), 64)), dim3(kNT), 0, st, r, s.lmin,
                            s.first_blk, nf);
     BCHECK(hipGetLastError());
+    tmark("memsets + edges + first_blk");
     size_t tb = s.temp_bytes;
     if (L > 0) {
         // ---- landmark order: stable sort by key = first-observing keyframe's id rank
@@ -456,6 +470,7 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
                            s.loc, s.info);
         BCHECK(hipGetLastError());
     }
+    tmark("landmark order");
     hipLaunchKernelGGL(k_b_lmcnt, dim3(grid(L + 1)), dim3(kNT), 0, st, s.lm_gpos, s.cnt, s.info, L, s.lc);
     BCHECK(hipGetLastError());
     tb = s.temp_bytes;
@@ -475,6 +490,7 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
         tb = s.temp_bytes;
         BCHECK(rocprim::radix_sort_pairs(s.temp, tb, s.pkey, s.pkey2, s.pval, s.pval2, (size_t)E, 0, bits_for(nf), st));
     }
+    tmark("edge CSR + pose sort");
     if (L) hipLaunchKernelGGL(k_b_states, dim3(grid(L)), dim3(kNT), 0, st, r, s.lm_gpos, s.info, s.X);
     // free-pose CSR offsets from the sorted pose keys (non-free edges carry key nf, sorted last)
     if (E) hipLaunchKernelGGL(k_b_lbound, dim3(grid((int64_t)nf + 1)), dim3(kNT), 0, st, s.pkey2, (int64_t)E, nf, s.pe_off);
@@ -490,6 +506,7 @@ int build_stage1(BuildMem &A, WindowBuild &wb, char *err, size_t errlen) {
     BCHECK(hipMemcpyAsync(&bad, s.err, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (nf) BCHECK(hipMemcpyAsync(wb.first_blk.data(), s.first_blk, sizeof(int32_t) * nf, hipMemcpyDeviceToHost, st));
     BCHECK(hipStreamSynchronize(st));
+    tmark("states + summary + readback");
     if (bad != kBig) {
         wb.invalid = true;
         snprintf(err, errlen, "%s edge %d references a missing vertex", bad < Ep ? "point" : "line", bad < Ep ? bad : bad - Ep);
