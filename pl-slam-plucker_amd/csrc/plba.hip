@@ -1302,7 +1302,7 @@ int do_upload(plba_ctx *ctx, const plba_graph *g) {
         // one staging block: Tcw | pt_xyz | ln_orth | χ² (doubles), then the byte outputs
         ALLOC(ctx->d_outd, out_doubles(n_kf, n_pt, n_ln, E) + ((size_t)Ep + E + 7) / 8);
     }
-#if defined(PLBA_STAMPS) || defined(PLBA_PHASE_STAMPS)
+#if defined(PLBA_STAMPS) || defined(PLBA_PHASE_STAMPS) || defined(PLBA_LMS_STAMPS)
     ZALLOC(d.stamps, 17 * 8);
 #endif
 #undef ALLOC
@@ -2372,7 +2372,7 @@ int plba_kernel_times(plba_ctx *ctx, const char **names, double *ms, int32_t *la
 
 // Diagnostic build only: per-wave, per-phase cycle sums of the banded factorisation.
 int plba_debug_stamps(plba_ctx *ctx, unsigned long long *out /* [17][8] */) {
-#if defined(PLBA_STAMPS) || defined(PLBA_PHASE_STAMPS)
+#if defined(PLBA_STAMPS) || defined(PLBA_PHASE_STAMPS) || defined(PLBA_LMS_STAMPS)
     if (!ctx || !ctx->d.stamps) return PLBA_E_STATE;
     PLBA_CHECK(d2h(ctx, out, ctx->d.stamps, 17 * 8 * sizeof(unsigned long long)));
     return PLBA_OK;

@@ -3250,6 +3250,12 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
         return;
     }
     const Dev d = slot_view(d0, (int)blockIdx.y);
+#ifdef PLBA_LMS_STAMPS  // diagnostic build only: per-workgroup phase times (d.stamps row 15)
+#define LMS_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#else
+#define LMS_T(v)
+#endif
+    LMS_T(lt0);
     const int gt = blockIdx.x * kLmsNT + threadIdx.x;
     const int l = gt / kLmLanes, q = gt % kLmLanes;   // a quad never straddles a wave
     const bool live = l < d.n_lm;
@@ -3315,6 +3321,7 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = quad_sum(u[i]);  // all lanes: DPP reads the whole quad
+    LMS_T(lt1);
     if (cg->hlm == 2) {
         u45[0] = quad_sum(u45[0]);
         u45[1] = quad_sum(u45[1]);
@@ -3487,14 +3494,34 @@ __global__ __launch_bounds__(kLmsNT) void k_lm_solve(Dev d0) {
             }
         }
     }
+    LMS_T(lt2);
     const double s2 = block_sum<kLmsNT>(sc, sh);
     const double s1 = block_sum<kLmsNT>(chi, sh);
     if (threadIdx.x == 0) {
         st_sc1(d.part_lms + blockIdx.x, s2);
         st_sc1(d.part_lm + blockIdx.x, s1);
     }
+    LMS_T(lt3);
     // the last workgroup to finish takes the trial decision (k_decide's work)
+#ifdef PLBA_LMS_STAMPS
+    const bool lms_last = d.fold && arrive_last(d.cnt, (int32_t)(gridDim.x * gridDim.y));
+    LMS_T(lt4);
+    if (lms_last) decide_body<kLmsNT>(d0, sh);
+    LMS_T(lt5);
+    if (threadIdx.x == 0 && d.stamps) {
+        unsigned long long *st = d.stamps + 15 * 8;
+        atomicAdd(st + 0, lt1 - lt0);
+        atomicAdd(st + 1, lt2 - lt1);
+        atomicAdd(st + 2, lt3 - lt2);
+        atomicAdd(st + 3, lt4 - lt3);
+        if (lms_last) atomicAdd(st + 4, lt5 - lt4);
+        atomicAdd(st + 5, 1ull);
+        atomicAdd(st + 6, lt4 - lt0);
+        if (lms_last) atomicAdd(st + 7, 1ull);
+    }
+#else
     if (d.fold && arrive_last(d.cnt, (int32_t)(gridDim.x * gridDim.y))) decide_body<kLmsNT>(d0, sh);
+#endif
 }
 // sharded: this rank's trial χ² and landmark scale terms into the all-reduced decision array
 __global__ __launch_bounds__(kBlock) void k_decide_pack(Dev d) {
